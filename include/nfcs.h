@@ -1,0 +1,162 @@
+/*
+ * nfcs.h — C ABI of the MI355X batched Internet-checksum engine.
+ *
+ * This is the drop-in boundary for NetFlow++'s checksum path:
+ *
+ *   netflow::Packet::update_checksums()      include/netflow++/packet.hpp:722-890
+ *   netflow::Packet::calculate_checksum()    include/netflow++/packet.hpp:894-912
+ *
+ * The reference exposes the path as a non-virtual inline C++ member that works on ONE
+ * packet in a PacketBuffer (packet_buffer.hpp:10-111). This ABI exposes the same
+ * computation over a BATCH of frames laid out in one arena (device or pinned host memory)
+ * and described by 8-byte descriptors. Every function returns an int status (0 = OK,
+ * < 0 = error; see nfcs_strerror) and never throws across the ABI. Per-packet results are
+ * written in place into the frames exactly as the reference writes them (bit-exact,
+ * including its quirks — SURVEY.md Appendix A), plus an optional per-packet status byte
+ * that records which branch of update_checksums() ran (the reference returns void and
+ * silently skips malformed packets: packet.hpp:758,763,780,784,786,791-793,830,834-836).
+ *
+ * No torch / HIP types appear in the signatures: streams are passed as void* (a
+ * hipStream_t, or NULL for the context's own stream).
+ */
+#ifndef NFCS_H
+#define NFCS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define NFCS_API __attribute__((visibility("default")))
+#else
+#define NFCS_API
+#endif
+
+#define NFCS_ABI_VERSION 1
+
+/* ---- data layout ------------------------------------------------------------------ */
+
+/* One frame inside an arena: bytes arena[off16*16, off16*16 + len).
+ * Replaces PacketBuffer's data window [get_data_start_ptr(), +get_data_length())
+ * (packet_buffer.hpp:51-52). Frames start on 16-byte boundaries; the arena must cover
+ * off16*16 + round_up(len, 16) bytes for every descriptor (the kernel reads whole 16-byte
+ * chunks; a descriptor outside the arena is rejected per packet with NFCS_ST_BAD_DESC). */
+typedef struct nfcs_desc {
+    uint32_t off16; /* frame start, in 16-byte units from the arena base */
+    uint32_t len;   /* frame length in bytes (PacketBuffer::data_len_)     */
+} nfcs_desc;
+
+/* ---- per-packet status (which branch of update_checksums() ran) -------------------- */
+enum {
+    NFCS_ST_NONE = 0,       /* neither IPv4 (by version nibble) nor IPv6: untouched (packet.hpp:761-765) */
+    NFCS_ST_V4 = 1,         /* IPv4 header checksum written; protocol not TCP/UDP/ICMP              */
+    NFCS_ST_V4_TCP = 2,     /* IPv4 header + TCP checksum (TCP field at l4+15, packet.hpp:258-270)  */
+    NFCS_ST_V4_UDP = 3,     /* IPv4 header + UDP checksum                                            */
+    NFCS_ST_V4_ICMP = 4,    /* IPv4 header + ICMP checksum                                           */
+    NFCS_ST_V4_L4SKIP = 5,  /* IPv4 header written; TCP/UDP/ICMP branch returned early (bounds)    */
+    NFCS_ST_V6 = 6,         /* IPv6 detected, next header neither TCP nor UDP: untouched            */
+    NFCS_ST_V6_TCP = 7,     /* IPv6 TCP checksum                                                     */
+    NFCS_ST_V6_UDP = 8,     /* IPv6 UDP checksum                                                     */
+    NFCS_ST_V6_L4SKIP = 9,  /* IPv6 TCP/UDP branch returned early (bounds): untouched                */
+    NFCS_ST_OOB = 14,       /* IPv4 with l2 + IHL*4 > len: the reference reads past the frame (UB);
+                               outside the parity domain, frame left untouched                      */
+    NFCS_ST_BAD_DESC = 15,  /* descriptor reaches past arena_bytes: frame not touched                */
+    NFCS_ST_FLAG_OVERLAP = 0x40 /* OR-ed in: IPv4 IHL < 5 with TCP/UDP/ICMP, so the L4 region
+                                   overlaps the IPv4 header; handled by the exact sequential path */
+};
+
+/* ---- error codes -------------------------------------------------------------------- */
+enum {
+    NFCS_OK = 0,
+    NFCS_EINVAL = -1,   /* bad argument (null pointer with n > 0, misaligned arena, ...) */
+    NFCS_EHIP = -2,     /* a HIP runtime call failed; nfcs_last_hip_error() has the code  */
+    NFCS_ENOMEM = -3,   /* allocation failed                                              */
+    NFCS_ENODEV = -4    /* no such device / no gfx950 device                              */
+};
+
+/* Synthetic workload configurations (BASELINE.json "configs"). */
+enum {
+    NFCS_CFG_C0_64B_V4 = 0,   /* 64 B IPv4, protocol 253 (header checksum only)   */
+    NFCS_CFG_C1_1500B_UDP = 1,/* 1500 B IPv4 + UDP                                 */
+    NFCS_CFG_C2_9000B_TCP = 2,/* 9000 B IPv4 + TCP                                 */
+    NFCS_CFG_C3_MIXED = 3     /* U{64..1500} B, 50/50 IPv4 TCP/UDP                 */
+};
+
+typedef struct nfcs_ctx nfcs_ctx;
+
+/* ---- library / context ---------------------------------------------------------------- */
+NFCS_API int nfcs_abi_version(void);
+NFCS_API const char* nfcs_strerror(int err);
+NFCS_API int nfcs_last_hip_error(void);
+
+/* One context per device: owns a stream, events and the pinned staging ring used by
+ * nfcs_update_host. Calls on one context must be serialised by the caller. */
+NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out);
+NFCS_API int nfcs_ctx_destroy(nfcs_ctx* ctx);
+NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t */
+
+/* ---- the hot path --------------------------------------------------------------------- */
+
+/* Batched Packet::update_checksums() on device-resident frames (packet.hpp:722-890).
+ *   d_arena      device pointer, 16-byte aligned, frames mutated in place
+ *   arena_bytes  size of the arena in bytes (descriptors are checked against it)
+ *   d_desc       n device-resident descriptors
+ *   d_status     optional (NULL) n status bytes, NFCS_ST_*
+ *   d_result     optional (NULL) n words: (ipv4_csum << 16) | l4_csum, each the 16-bit
+ *                value as stored big-endian in the frame; 0 where nothing was written
+ *   stream       hipStream_t or NULL (context stream). Asynchronous: completion is
+ *                observed by synchronising the stream. */
+NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                                const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
+                                uint32_t* d_result, void* stream);
+
+/* Same on host memory (NIC / socket buffers). Frames are staged through the context's
+ * pinned ring in chunks (H2D copy, kernel, D2H copy overlapped on two streams) and the
+ * updated bytes are written back into h_arena. Synchronous. h_arena need not be pinned;
+ * pinned memory (nfcs_host_alloc) avoids one host-side copy. */
+NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
+                              const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status);
+
+/* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
+
+/* Lay out n frames of a config (packet indices first_index .. first_index+n-1) with
+ * 16-byte aligned starts; fills h_desc (may be NULL) and returns the arena bytes needed
+ * through *arena_bytes. Pure host code. */
+NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
+                                nfcs_desc* h_desc, uint64_t* arena_bytes);
+
+/* Fill the frames of a laid-out config batch on the device (d_desc from nfcs_layout_config). */
+NFCS_API int nfcs_gen_config_device(nfcs_ctx* ctx, int config, uint64_t seed,
+                                    uint64_t first_index, uint32_t n, uint8_t* d_arena,
+                                    uint64_t arena_bytes, const nfcs_desc* d_desc, void* stream);
+
+/* Order-independent 64-bit digest of the n frames (packet index first_index + i):
+ *   digest = sum_i mix64(frame_hash(frame_i) ^ ((first_index + i) * 0xA0761D6478BD642F))
+ * (DESIGN.md §6 gives frame_hash). Synchronous; result in *h_digest. */
+NFCS_API int nfcs_digest_device(nfcs_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                                const nfcs_desc* d_desc, uint32_t n, uint64_t first_index,
+                                uint64_t* h_digest, void* stream);
+
+/* ---- memory helpers for callers without their own HIP runtime ------------------------- */
+NFCS_API int nfcs_device_alloc(nfcs_ctx* ctx, size_t bytes, void** out);
+NFCS_API int nfcs_device_free(nfcs_ctx* ctx, void* p);
+NFCS_API int nfcs_host_alloc(nfcs_ctx* ctx, size_t bytes, void** out); /* pinned */
+NFCS_API int nfcs_host_free(nfcs_ctx* ctx, void* p);
+NFCS_API int nfcs_memcpy_h2d(nfcs_ctx* ctx, void* dst, const void* src, size_t bytes);
+NFCS_API int nfcs_memcpy_d2h(nfcs_ctx* ctx, void* dst, const void* src, size_t bytes);
+NFCS_API int nfcs_stream_sync(nfcs_ctx* ctx, void* stream);
+
+/* ---- timing (bench support): HIP events on the given stream ---------------------------- */
+/* Time `iters` back-to-back nfcs_update_device launches on `stream` with HIP events recorded
+ * on that same stream; returns total milliseconds in *ms. */
+NFCS_API int nfcs_time_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                                     const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
+                                     int iters, void* stream, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFCS_H */

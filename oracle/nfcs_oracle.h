@@ -1,0 +1,64 @@
+/*
+ * nfcs_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of NetFlow++'s Packet::update_checksums() (packet.hpp:722-912) used as the
+ * parity checker for the HIP engine. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (netflow_amd / libnfcs.so) never links it.
+ *
+ * Parity pinning: this restatement is checked against the reference itself — the
+ * reference header compiled from /root/reference by oracle/Makefile into oracle/_ref/ —
+ * on the Appendix-B known-answer frames and on a fuzz corpus; the committed fixtures in
+ * tests/golden/ were produced by the compiled reference (tests/golden/make_golden.py).
+ */
+#ifndef NFCS_ORACLE_H
+#define NFCS_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes: identical values to include/nfcs.h NFCS_ST_* (checked by tests) */
+enum {
+    NFO_ST_NONE = 0, NFO_ST_V4 = 1, NFO_ST_V4_TCP = 2, NFO_ST_V4_UDP = 3, NFO_ST_V4_ICMP = 4,
+    NFO_ST_V4_L4SKIP = 5, NFO_ST_V6 = 6, NFO_ST_V6_TCP = 7, NFO_ST_V6_UDP = 8,
+    NFO_ST_V6_L4SKIP = 9, NFO_ST_OOB = 14, NFO_ST_BAD_DESC = 15, NFO_ST_FLAG_OVERLAP = 0x40
+};
+
+typedef struct nfo_desc { uint32_t off16; uint32_t len; } nfo_desc;
+
+/* one frame, in place; returns the status byte */
+int nfo_update(uint8_t* frame, size_t len);
+/* Packet::calculate_checksum (packet.hpp:894-912): returns the 16-bit value that the
+ * reference stores big-endian (i.e. ntohs of the stored field) */
+uint16_t nfo_calculate_checksum(const uint8_t* data, size_t len);
+/* batch over an arena; status may be NULL; returns 0 */
+int nfo_update_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc, uint32_t n,
+                     uint8_t* status, uint32_t* result, int nthreads);
+
+/* synthetic configs (spec in DESIGN.md §6) */
+uint32_t nfo_config_len(int config, uint64_t seed, uint64_t index);
+void nfo_config_frame(int config, uint64_t seed, uint64_t index, uint8_t* out /* >= len */);
+uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n, nfo_desc* desc);
+void nfo_gen_config(int config, uint64_t seed, uint64_t first, uint32_t n, uint8_t* arena,
+                    const nfo_desc* desc);
+
+/* fuzz corpus frames (edge cases: VLAN, IHL 0-15, IPv6, ICMP, truncation, bad lengths,
+ * odd lengths, jumbo). Returns len (<= 9000); out must hold 9016 bytes. */
+uint32_t nfo_fuzz_frame(uint64_t seed, uint64_t index, uint8_t* out);
+
+/* digests (order-independent) */
+uint64_t nfo_mix64(uint64_t z);
+uint64_t nfo_frame_hash(const uint8_t* frame, uint32_t len);
+uint64_t nfo_digest(const uint8_t* arena, const nfo_desc* desc, uint32_t n, uint64_t first);
+/* streaming: generate packets [first, first+n) of a config, digest them before and after
+ * nfo_update, count statuses; multi-threaded; O(1) memory per thread */
+void nfo_config_digest(int config, uint64_t seed, uint64_t first, uint64_t n, int nthreads,
+                       uint64_t* digest_in, uint64_t* digest_out, uint64_t* status_hist /*[256]*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

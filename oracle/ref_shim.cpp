@@ -1,0 +1,85 @@
+// ref_shim.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Exposes the REFERENCE implementation of the checksum path through a C ABI so that tests
+// and the golden-fixture script can run it. The reference source is NOT copied: this file
+// is compiled against /root/reference/include by oracle/Makefile (target `ref`), and the
+// result goes to oracle/_ref/libnfref.so (git-ignored). The path is header-only
+// (include/netflow++/packet.hpp + packet_buffer.hpp) and needs nothing but libc/libstdc++.
+//
+// Calls netflow::Packet::update_checksums() (packet.hpp:722-890) on a PacketBuffer
+// (packet_buffer.hpp:10-111) whose data window is pointed at the caller's frame, so the
+// reference mutates the caller's bytes in place exactly as it would its own buffer.
+#include <netflow++/packet.hpp>
+
+#include <cstdint>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Window {
+    netflow::PacketBuffer pb;
+    unsigned char* own;
+    Window() : pb(16, 0, 0), own(pb.raw_data_ptr_) {}
+    ~Window() { pb.raw_data_ptr_ = own; }  // the PacketBuffer dtor deletes its own bytes
+    void point(uint8_t* frame, size_t len) {
+        pb.raw_data_ptr_ = frame;
+        pb.capacity_ = len;
+        pb.data_offset_ = 0;
+        pb.data_len_ = len;
+    }
+};
+
+struct Desc { uint32_t off16; uint32_t len; };
+
+}  // namespace
+
+extern "C" {
+
+// One frame, in place. The caller guarantees the frame is in the reference's defined
+// domain (an IPv4 header whose IHL*4 reaches past len makes the reference read past it).
+__attribute__((visibility("default"))) void nfref_update(uint8_t* frame, size_t len) {
+    Window w;
+    w.point(frame, len);
+    netflow::Packet pkt(&w.pb);  // increments the refcount like every reference caller
+    pkt.update_checksums();
+}
+
+// Batch over an arena: one Packet per frame on `nthreads` std::threads (contiguous static
+// slices). This is the reference's own per-packet code path and cost structure (per-call
+// std::vector pseudo-header+segment copy, scalar ntohs fold), used as the CPU baseline.
+__attribute__((visibility("default"))) void nfref_update_batch(uint8_t* arena, const void* desc_v,
+                                                               uint32_t n, int nthreads) {
+    const Desc* desc = static_cast<const Desc*>(desc_v);
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](uint32_t lo, uint32_t hi) {
+        Window w;
+        for (uint32_t i = lo; i < hi; ++i) {
+            w.point(arena + (uint64_t)desc[i].off16 * 16, desc[i].len);
+            netflow::Packet pkt(&w.pb);
+            pkt.update_checksums();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t)
+        th.emplace_back(work, (uint32_t)((uint64_t)n * t / nthreads),
+                        (uint32_t)((uint64_t)n * (t + 1) / nthreads));
+    work(0, (uint32_t)((uint64_t)n / nthreads));
+    for (auto& t : th) t.join();
+}
+
+__attribute__((visibility("default"))) int nfref_struct_sizes(int which) {
+    switch (which) {
+    case 0: return (int)sizeof(netflow::EthernetHeader);
+    case 1: return (int)sizeof(netflow::VlanHeader);
+    case 2: return (int)sizeof(netflow::IPv4Header);
+    case 3: return (int)sizeof(netflow::IPv6Header);
+    case 4: return (int)sizeof(netflow::TcpHeader);
+    case 5: return (int)sizeof(netflow::UdpHeader);
+    case 6: return (int)sizeof(netflow::IcmpHeader);
+    case 7: return (int)offsetof(netflow::TcpHeader, checksum);
+    default: return -1;
+    }
+}
+
+}  // extern "C"
