@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident batched checksum throughput (BASELINE.json metric).
+
+A "step" is one pass of the hot path — NetFlow++'s Packet::update_checksums()
+(packet.hpp:722-890), batched on the gfx950 engine — over one batch of synthetic frames that
+is already resident in HBM. At N=1 the workload is BASELINE config C1 (1 M x 1500 B IPv4+UDP
+on 1 MI355X); with --gpus N each rank owns its own C1 batch (packets [rank*n, (rank+1)*n)),
+so per-GPU work is fixed (weak scaling) and there is no collective on the data path: ranks
+only meet at the timing barriers.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1] [--packets n] [--no-cpu]
+
+Prints ONE JSON line on rank 0. `value` = sum over ranks of frame bytes per step / the max
+over ranks of the timed wall time per step. `roofline` uses the kernel's HIP-event time on its
+own stream; `cpu_baseline` times the reference update_checksums() (oracle/_ref, compiled from
+/root/reference) or, if that .so is absent, the oracle port, on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import netflow_amd as nf  # noqa: E402
+
+SEED = 20250620
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip parameters)
+DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
+WORKLOAD = {
+    0: "C0: 1024 x 64 B IPv4 (header checksum only)",
+    1: "C1: 1M x 1500 B IPv4+UDP, device-resident",
+    2: "C2: 1M x 9000 B IPv4+TCP jumbo, device-resident",
+    3: "C3: 4M x U{64..1500} B IPv4 TCP/UDP mix, device-resident",
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Dist:
+    """Barrier + max-over-ranks. Uses torch.distributed (RCCL via backend 'nccl' when GPUs
+    are visible to torch, else gloo); a no-op at world size 1."""
+
+    def __init__(self, ws, rank, local):
+        self.ws, self.rank, self.local = ws, rank, local
+        self.pg = None
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            backend = os.environ.get("NFCS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+            dist.init_process_group(backend=backend)
+            self.dist, self.torch, self.backend = dist, torch, backend
+
+    def _t(self, v):
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        return t.cuda() if self.backend == "nccl" else t
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.all_reduce(self._t(0.0))
+
+    def max(self, v: float) -> float:
+        if self.ws == 1:
+            return float(v)
+        t = self._t(v)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.ws == 1:
+            return float(v)
+        t = self._t(v)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.destroy_process_group()
+
+
+def device_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def shard(rank: int, n_per_rank: int) -> tuple[int, int]:
+    """Packet index range of a rank (weak scaling: every rank owns n_per_rank packets)."""
+    return rank * n_per_rank, n_per_rank
+
+
+def golden_digest(config: int, first: int, n: int):
+    try:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+    except OSError:
+        return None
+    c = g["configs"].get(str(config))
+    if c and c["first"] == first and c["n"] == n:
+        return c["digest_out"]
+    if config == 1:
+        for sh in g.get("c1_rank_shards", []):
+            if sh["first"] == first and sh["n"] == n:
+                return sh["digest_out"]
+    return None
+
+
+def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0):
+    """Reference update_checksums() on host cores over a bounded sample of the workload."""
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "error": repr(e)}
+    kind = "reference" if oracle.ref_available() else "port"
+    n = {0: 1024, 1: 1 << 17, 2: 1 << 14, 3: 1 << 17}[config]
+    arena, desc = oracle.gen_config(config, SEED, 0, n)
+    nbytes = float(desc["len"].astype(np.float64).sum())
+    if kind == "reference":
+        R = oracle.ref()
+        run = lambda: R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, n, threads)
+    else:
+        L = oracle.lib()
+        run = lambda: L.nfo_update_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
+                                         None, None, threads)
+    run()  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    gbs = nbytes * reps / el / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes, "
+                      f"{threads} threads, g++ -O2, {el:.1f} s"}
+
+
+def load_traffic(config: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        t = json.load(open(p))
+        return t.get(f"C{config}")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=1, choices=[0, 1, 2, 3])
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config size)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    D = Dist(ws, rank, local)
+    n = args.packets or DEFAULT_PACKETS[args.config]
+    first, n = shard(rank, n)
+
+    eng = nf.Engine(local)
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n)
+    frame_bytes = float(hdesc["len"].astype(np.float64).sum())
+    algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
+
+    for _ in range(args.warmup):
+        eng.update_device(d_arena, nbytes, d_desc, n)
+    eng.sync()
+
+    # timed region: barrier + device sync on both sides, max over ranks
+    D.barrier()
+    device_sync()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.update_device(d_arena, nbytes, d_desc, n)
+    eng.sync()
+    device_sync()
+    t1 = time.perf_counter()
+    D.barrier()
+    wall = D.max(t1 - t0)
+    ms_per_step = wall / args.steps * 1e3
+    total_frame_bytes = D.sum(frame_bytes)
+
+    # kernel duration with HIP events on the launch stream (roofline), same launches
+    ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
+    achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
+
+    # parity of what was measured: digest of the updated arena vs the reference's
+    want = golden_digest(args.config, first, n)
+    got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
+    parity_ok = None if want is None else (got == want)
+    parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
+
+    traffic = load_traffic(args.config)
+    out = {
+        "metric": "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X",
+        "value": round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16 one's-complement (u8 frames, u64 accumulate)",
+        "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
+        "config": {"workload": WORKLOAD[args.config], "packets_per_gpu": n,
+                   "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(ev_ms, 4),
+                     "algorithmic_bytes_per_launch": int(algo_bytes)},
+        "parity": {"digest": got, "reference_digest": want, "match": parity_ok, "all_ranks": parity_all},
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    d_arena.free()
+    eng.close()
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

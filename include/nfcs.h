@@ -49,6 +49,18 @@ typedef struct nfcs_desc {
     uint32_t len;   /* frame length in bytes (PacketBuffer::data_len_)     */
 } nfcs_desc;
 
+/* What update_checksums() wrote into one frame: at most two 2-byte fields. Applying
+ * ip then l4 to the original frame reproduces the updated frame exactly (also when the two
+ * fields overlap, IHL < 5). Offsets are frame offsets; 0xFFFF = field not written. */
+typedef struct nfcs_patch {
+    uint16_t ip_off;  /* IPv4 header checksum field: l2 + 10                         */
+    uint16_t l4_off;  /* L4 checksum field: TCP l4+15 (sic), UDP l4+6, ICMP l4+2     */
+    uint8_t ip[2];    /* bytes written at ip_off (big-endian checksum)               */
+    uint8_t l4[2];    /* bytes written at l4_off                                     */
+} nfcs_patch;
+
+#define NFCS_PATCH_NONE 0xFFFFu
+
 /* ---- per-packet status (which branch of update_checksums() ran) -------------------- */
 enum {
     NFCS_ST_NONE = 0,       /* neither IPv4 (by version nibble) nor IPv6: untouched (packet.hpp:761-765) */
@@ -105,20 +117,24 @@ NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t 
  *   arena_bytes  size of the arena in bytes (descriptors are checked against it)
  *   d_desc       n device-resident descriptors
  *   d_status     optional (NULL) n status bytes, NFCS_ST_*
- *   d_result     optional (NULL) n words: (ipv4_csum << 16) | l4_csum, each the 16-bit
- *                value as stored big-endian in the frame; 0 where nothing was written
+ *   d_patch      optional (NULL) n nfcs_patch records describing the bytes written
  *   stream       hipStream_t or NULL (context stream). Asynchronous: completion is
  *                observed by synchronising the stream. */
 NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
-                                uint32_t* d_result, void* stream);
+                                nfcs_patch* d_patch, void* stream);
 
 /* Same on host memory (NIC / socket buffers). Frames are staged through the context's
  * pinned ring in chunks (H2D copy, kernel, D2H copy overlapped on two streams) and the
  * updated bytes are written back into h_arena. Synchronous. h_arena need not be pinned;
- * pinned memory (nfcs_host_alloc) avoids one host-side copy. */
+ * pinned memory (nfcs_host_alloc) avoids one host-side copy. Descriptors must be sorted by
+ * off16 (frames in arena order, as a NIC ring or nfcs_layout_config lays them out).
+ * flags: NFCS_HOST_PATCH_ONLY copies back 8-byte nfcs_patch records instead of whole
+ * frames and applies them on the host. */
+#define NFCS_HOST_PATCH_ONLY 1u
 NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
-                              const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status);
+                              const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
+                              uint32_t flags);
 
 /* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
 

@@ -1,0 +1,230 @@
+"""netflow_amd — MI355X-native batched Internet-checksum engine for NetFlow++'s
+``Packet::update_checksums()`` path (include/netflow++/packet.hpp:722-912).
+
+The compute lives in ``libnfcs.so`` (hand-written gfx950 HIP kernels behind the C ABI in
+``include/nfcs.h``). This module is a thin ctypes host layer over that ABI: device buffers,
+contexts, the batched update on device-resident or host-resident frames, synthetic batches
+and digests. It never computes a checksum itself and has no CPU fallback: if the HIP
+library is missing or no gfx950 device is present, it raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libnfcs.so")
+HEADER = os.path.join(ROOT, "include", "nfcs.h")
+SOURCES = [os.path.join(HERE, "csrc", "nfcs_kernels.hip"), os.path.join(HERE, "csrc", "nfcs_api.hip")]
+
+DESC_DTYPE = np.dtype([("off16", "<u4"), ("len", "<u4")])
+PATCH_DTYPE = np.dtype([("ip_off", "<u2"), ("l4_off", "<u2"), ("ip", "u1", (2,)), ("l4", "u1", (2,))])
+
+# status codes (include/nfcs.h)
+ST_NONE, ST_V4, ST_V4_TCP, ST_V4_UDP, ST_V4_ICMP, ST_V4_L4SKIP = 0, 1, 2, 3, 4, 5
+ST_V6, ST_V6_TCP, ST_V6_UDP, ST_V6_L4SKIP, ST_OOB, ST_BAD_DESC = 6, 7, 8, 9, 14, 15
+ST_FLAG_OVERLAP = 0x40
+CFG_C0, CFG_C1, CFG_C2, CFG_C3 = 0, 1, 2, 3
+HOST_PATCH_ONLY = 1
+PATCH_NONE = 0xFFFF
+
+
+class NfcsError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree)."""
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"),
+           *SOURCES, "-o", LIB_PATH]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+
+def _declare(L):
+    sig = {
+        "nfcs_abi_version": ([], ctypes.c_int),
+        "nfcs_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "nfcs_last_hip_error": ([], ctypes.c_int),
+        "nfcs_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
+        "nfcs_ctx_destroy": ([_vp], ctypes.c_int),
+        "nfcs_ctx_stream": ([_vp], _vp),
+        "nfcs_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
+        "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
+        "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
+        "nfcs_gen_config_device": ([_vp, ctypes.c_int, _u64, _u64, _u32, _vp, _u64, _vp, _vp], ctypes.c_int),
+        "nfcs_digest_device": ([_vp, _vp, _u64, _vp, _u32, _u64, ctypes.POINTER(_u64), _vp], ctypes.c_int),
+        "nfcs_device_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+        "nfcs_device_free": ([_vp, _vp], ctypes.c_int),
+        "nfcs_host_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+        "nfcs_host_free": ([_vp, _vp], ctypes.c_int),
+        "nfcs_memcpy_h2d": ([_vp, _vp, _vp, ctypes.c_size_t], ctypes.c_int),
+        "nfcs_memcpy_d2h": ([_vp, _vp, _vp, ctypes.c_size_t], ctypes.c_int),
+        "nfcs_stream_sync": ([_vp, _vp], ctypes.c_int),
+        "nfcs_time_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, ctypes.c_int, _vp,
+                                     ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+def lib() -> ctypes.CDLL:
+    """Load libnfcs.so. Raises if the HIP library has not been built: there is no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NfcsError(f"{LIB_PATH} is missing: build it with netflow_amd.build() "
+                            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        _lib = _declare(ctypes.CDLL(LIB_PATH))
+        if _lib.nfcs_abi_version() != 1:
+            raise NfcsError("libnfcs.so ABI mismatch")
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        L = lib()
+        raise NfcsError(f"{what}: {L.nfcs_strerror(rc).decode()} (rc={rc}, hip={L.nfcs_last_hip_error()})")
+
+
+def layout_config(config: int, seed: int, first: int, n: int):
+    """Descriptors of n synthetic frames of `config` (16-byte aligned, arena order)."""
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    nbytes = _u64()
+    _check(lib().nfcs_layout_config(config, seed, first, n, desc.ctypes.data if n else None,
+                                    ctypes.byref(nbytes)), "nfcs_layout_config")
+    return desc, int(nbytes.value)
+
+
+class DeviceBuffer:
+    """A raw device allocation owned by an Engine (no torch types involved)."""
+
+    def __init__(self, engine: "Engine", nbytes: int):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = _vp()
+        _check(lib().nfcs_device_alloc(engine.ctx, max(self.nbytes, 16), ctypes.byref(p)), "device_alloc")
+        self.ptr = p.value
+
+    def upload(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        if a.nbytes:
+            _check(lib().nfcs_memcpy_h2d(self.engine.ctx, self.ptr, a.ctypes.data, a.nbytes), "h2d")
+        return self
+
+    def download(self, dtype=np.uint8, count: int | None = None) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        count = self.nbytes // dtype.itemsize if count is None else count
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            _check(lib().nfcs_memcpy_d2h(self.engine.ctx, out.ctypes.data, self.ptr, out.nbytes), "d2h")
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().nfcs_device_free(self.engine.ctx, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One nfcs context on one device (nfcs_ctx_create)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        c = _vp()
+        _check(lib().nfcs_ctx_create(device, ctypes.byref(c)), f"nfcs_ctx_create({device})")
+        self.ctx = c.value
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib().nfcs_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self) -> int:
+        return lib().nfcs_ctx_stream(self.ctx)
+
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def sync(self, stream=None):
+        _check(lib().nfcs_stream_sync(self.ctx, stream), "stream_sync")
+
+    # ---- the hot path -------------------------------------------------------------------
+    def update_device(self, arena: DeviceBuffer | int, arena_bytes: int, desc: DeviceBuffer | int,
+                      n: int, status=None, patch=None, stream=None):
+        """Batched update_checksums() on device-resident frames (async on `stream`)."""
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_update_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n,
+                                        ptr(status), ptr(patch), stream), "nfcs_update_device")
+
+    def update_host(self, arena: np.ndarray, desc: np.ndarray, want_status: bool = True,
+                    patch_only: bool = False) -> np.ndarray | None:
+        """Batched update_checksums() on host frames (in place); returns status bytes."""
+        assert arena.dtype == np.uint8 and arena.flags.c_contiguous
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        n = len(desc)
+        status = np.zeros(n, dtype=np.uint8) if want_status else None
+        _check(lib().nfcs_update_host(self.ctx, arena.ctypes.data, arena.nbytes,
+                                      desc.ctypes.data if n else None, n,
+                                      status.ctypes.data if want_status and n else None,
+                                      HOST_PATCH_ONLY if patch_only else 0), "nfcs_update_host")
+        return status
+
+    def time_update_device(self, arena, arena_bytes, desc, n, iters, status=None, stream=None) -> float:
+        ms = ctypes.c_float()
+        _check(lib().nfcs_time_update_device(self.ctx, arena.ptr, arena_bytes, desc.ptr, n,
+                                             None if status is None else status.ptr, iters, stream,
+                                             ctypes.byref(ms)), "time_update_device")
+        return float(ms.value)
+
+    # ---- synthetic batches / digests ----------------------------------------------------
+    def gen_config_device(self, config: int, seed: int, first: int, n: int,
+                          arena: DeviceBuffer, arena_bytes: int, desc: DeviceBuffer, stream=None):
+        _check(lib().nfcs_gen_config_device(self.ctx, config, seed, first, n, arena.ptr, arena_bytes,
+                                            desc.ptr, stream), "gen_config_device")
+
+    def digest_device(self, arena: DeviceBuffer, arena_bytes: int, desc: DeviceBuffer, n: int,
+                      first: int = 0, stream=None) -> int:
+        out = _u64()
+        _check(lib().nfcs_digest_device(self.ctx, arena.ptr, arena_bytes, desc.ptr, n, first,
+                                        ctypes.byref(out), stream), "digest_device")
+        return int(out.value)
+
+    def config_batch(self, config: int, seed: int, first: int, n: int):
+        """Lay out + generate a synthetic batch on the device. Returns (arena, nbytes, desc, host_desc)."""
+        hdesc, nbytes = layout_config(config, seed, first, n)
+        d_desc = self.alloc(max(hdesc.nbytes, 16)).upload(hdesc)
+        d_arena = self.alloc(max(nbytes, 16))
+        self.gen_config_device(config, seed, first, n, d_arena, nbytes, d_desc)
+        self.sync()
+        return d_arena, nbytes, d_desc, hdesc

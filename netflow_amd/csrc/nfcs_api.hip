@@ -1,0 +1,370 @@
+// nfcs_api.hip — the C ABI (include/nfcs.h) over the gfx950 kernels: per-device context,
+// argument checking, the device-resident entry point, the host-memory pipeline (pinned
+// staging ring, H2D / kernel / D2H overlapped on two streams), synthetic batches, digests.
+//
+// Boundary being replaced: netflow::Packet::update_checksums() (packet.hpp:722-890), a void
+// member that never throws and silently skips malformed packets. Here every entry point returns
+// an int (0 or a negative NFCS_E*), never throws, and reports per-packet outcomes as status bytes.
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "nfcs_internal.h"
+
+struct nfcs_ctx {
+    nfcs::DevInfo di;
+    hipStream_t stream = nullptr;
+    // host pipeline (nfcs_update_host)
+    static constexpr int kSlots = 2;
+    hipStream_t hs[kSlots] = {nullptr, nullptr};
+    hipEvent_t done[kSlots] = {nullptr, nullptr};
+    size_t stage_bytes = 0;   // arena bytes per slot
+    uint32_t stage_pkts = 0;  // descriptors per slot
+    uint8_t* d_arena[kSlots] = {nullptr, nullptr};
+    nfcs_desc* d_desc[kSlots] = {nullptr, nullptr};
+    uint8_t* d_status[kSlots] = {nullptr, nullptr};
+    nfcs_patch* d_patch[kSlots] = {nullptr, nullptr};
+    uint8_t* h_arena[kSlots] = {nullptr, nullptr};  // pinned
+    nfcs_desc* h_desc[kSlots] = {nullptr, nullptr};
+    uint8_t* h_status[kSlots] = {nullptr, nullptr};
+    nfcs_patch* h_patch[kSlots] = {nullptr, nullptr};
+    uint64_t* d_digest = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int variant = 0;
+    int grid = 0;
+};
+
+namespace {
+
+thread_local int g_last_hip = 0;
+
+int hip_fail(hipError_t e) {
+    g_last_hip = (int)e;
+    return NFCS_EHIP;
+}
+#define NFCS_HIP(x)                              \
+    do {                                         \
+        hipError_t e_ = (x);                     \
+        if (e_ != hipSuccess) return hip_fail(e_); \
+    } while (0)
+
+hipStream_t pick(nfcs_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+int ensure_host_pipeline(nfcs_ctx* ctx) {
+    if (ctx->d_arena[0]) return NFCS_OK;
+    ctx->stage_bytes = (size_t)env_int("NFCS_STAGE_MB", 64) << 20;
+    ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
+    for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
+        NFCS_HIP(hipStreamCreateWithFlags(&ctx->hs[s], hipStreamNonBlocking));
+        NFCS_HIP(hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming));
+        NFCS_HIP(hipMalloc(&ctx->d_arena[s], ctx->stage_bytes));
+        NFCS_HIP(hipMalloc(&ctx->d_desc[s], (size_t)ctx->stage_pkts * sizeof(nfcs_desc)));
+        NFCS_HIP(hipMalloc(&ctx->d_status[s], ctx->stage_pkts));
+        NFCS_HIP(hipMalloc(&ctx->d_patch[s], (size_t)ctx->stage_pkts * sizeof(nfcs_patch)));
+        NFCS_HIP(hipHostMalloc(&ctx->h_arena[s], ctx->stage_bytes, hipHostMallocDefault));
+        NFCS_HIP(hipHostMalloc(&ctx->h_desc[s], (size_t)ctx->stage_pkts * sizeof(nfcs_desc),
+                               hipHostMallocDefault));
+        NFCS_HIP(hipHostMalloc(&ctx->h_status[s], ctx->stage_pkts, hipHostMallocDefault));
+        NFCS_HIP(hipHostMalloc(&ctx->h_patch[s], (size_t)ctx->stage_pkts * sizeof(nfcs_patch),
+                               hipHostMallocDefault));
+    }
+    return NFCS_OK;
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+}  // namespace
+
+extern "C" {
+
+NFCS_API int nfcs_abi_version(void) { return NFCS_ABI_VERSION; }
+
+NFCS_API const char* nfcs_strerror(int err) {
+    switch (err) {
+    case NFCS_OK: return "ok";
+    case NFCS_EINVAL: return "invalid argument";
+    case NFCS_EHIP: return "HIP runtime error";
+    case NFCS_ENOMEM: return "out of memory";
+    case NFCS_ENODEV: return "no gfx950 device";
+    default: return "unknown error";
+    }
+}
+
+NFCS_API int nfcs_last_hip_error(void) { return g_last_hip; }
+
+NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
+    if (!out) return NFCS_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        (void)hipGetLastError();
+        return NFCS_ENODEV;
+    }
+    NFCS_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    NFCS_HIP(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NFCS_ENODEV;
+    nfcs_ctx* c = new (std::nothrow) nfcs_ctx();
+    if (!c) return NFCS_ENOMEM;
+    c->di.device = device;
+    c->di.cus = prop.multiProcessorCount;
+    strncpy(c->di.arch, prop.gcnArchName, sizeof(c->di.arch) - 1);
+    c->variant = env_int("NFCS_VARIANT", 0);
+    c->grid = env_int("NFCS_GRID", 0);
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_digest, sizeof(uint64_t));
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        nfcs_ctx_destroy(c);
+        return hip_fail(e);
+    }
+    *out = c;
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
+    if (!c) return NFCS_OK;
+    (void)hipSetDevice(c->di.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
+        if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
+        if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+        (void)hipFree(c->d_arena[s]);
+        (void)hipFree(c->d_desc[s]);
+        (void)hipFree(c->d_status[s]);
+        (void)hipFree(c->d_patch[s]);
+        if (c->h_arena[s]) (void)hipHostFree(c->h_arena[s]);
+        if (c->h_desc[s]) (void)hipHostFree(c->h_desc[s]);
+        if (c->h_status[s]) (void)hipHostFree(c->h_status[s]);
+        if (c->h_patch[s]) (void)hipHostFree(c->h_patch[s]);
+    }
+    if (c->d_digest) (void)hipFree(c->d_digest);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return NFCS_OK;
+}
+
+NFCS_API void* nfcs_ctx_stream(nfcs_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
+                                nfcs_patch* d_patch, void* stream) {
+    if (!c) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
+    NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
+                                 pick(c, stream), c->variant, c->grid));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
+                              const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
+                              uint32_t flags) {
+    if (!c) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!h_arena || !h_desc) return NFCS_EINVAL;
+    for (uint32_t i = 1; i < n; ++i)
+        if (h_desc[i].off16 < h_desc[i - 1].off16) return NFCS_EINVAL;  // must be arena order
+    int rc = ensure_host_pipeline(c);
+    if (rc) return rc;
+    const bool patch_only = flags & NFCS_HOST_PATCH_ONLY;
+    const bool pinned = is_pinned(h_arena);
+
+    struct Chunk { uint32_t i0, i1; uint64_t base, bytes; bool used; };
+    Chunk slot[nfcs_ctx::kSlots] = {};
+
+    // finish a slot: wait for its D2H, then copy frames / apply patches / copy statuses
+    auto finish = [&](int s) -> int {
+        Chunk& k = slot[s];
+        if (!k.used) return NFCS_OK;
+        NFCS_HIP(hipEventSynchronize(c->done[s]));
+        const uint32_t m = k.i1 - k.i0;
+        if (patch_only) {
+            for (uint32_t i = 0; i < m; ++i) {
+                const nfcs_patch& pt = c->h_patch[s][i];
+                const uint64_t off = (uint64_t)h_desc[k.i0 + i].off16 * 16u;
+                if (off + h_desc[k.i0 + i].len > arena_bytes) continue;
+                uint8_t* f = h_arena + off;
+                if (pt.ip_off != NFCS_PATCH_NONE) { f[pt.ip_off] = pt.ip[0]; f[pt.ip_off + 1] = pt.ip[1]; }
+                if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
+            }
+        } else if (!pinned) {
+            memcpy(h_arena + k.base, c->h_arena[s], k.bytes);
+        }
+        if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
+        k.used = false;
+        return NFCS_OK;
+    };
+
+    uint32_t i = 0;
+    int s = 0;
+    while (i < n) {
+        // next chunk: packets [i0, i1) whose frames fit one staging slot
+        const uint64_t base = (uint64_t)h_desc[i].off16 * 16u;
+        uint32_t i1 = i;
+        uint64_t end = base;
+        while (i1 < n && i1 - i < c->stage_pkts) {
+            const uint64_t o = (uint64_t)h_desc[i1].off16 * 16u;
+            const uint64_t e = std::min<uint64_t>(o + (((uint64_t)h_desc[i1].len + 15u) & ~15ull),
+                                                  arena_bytes);
+            const uint64_t ne = std::max(end, e);
+            if (ne - base > c->stage_bytes) {
+                if (i1 == i) return NFCS_EINVAL;  // a single frame larger than a slot
+                break;
+            }
+            end = ne;
+            ++i1;
+        }
+        rc = finish(s);
+        if (rc) return rc;
+        Chunk& k = slot[s];
+        k = {i, i1, base, end - base, true};
+        const uint32_t m = i1 - i;
+        const uint8_t* src = h_arena + base;
+        if (!pinned) {
+            memcpy(c->h_arena[s], src, k.bytes);
+            src = c->h_arena[s];
+        }
+        memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        hipStream_t st = c->hs[s];
+        NFCS_HIP(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
+                                hipMemcpyHostToDevice, st));
+        NFCS_HIP(hipMemcpyAsync(c->d_arena[s], src, k.bytes, hipMemcpyHostToDevice, st));
+        NFCS_HIP(nfcs::launch_update(c->di, c->d_arena[s], k.bytes, c->d_desc[s], m,
+                                     (uint32_t)(base >> 4), c->d_status[s],
+                                     patch_only ? c->d_patch[s] : nullptr, st, c->variant,
+                                     c->grid));
+        if (patch_only) {
+            NFCS_HIP(hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
+                                    hipMemcpyDeviceToHost, st));
+        } else {
+            uint8_t* dst = pinned ? h_arena + base : c->h_arena[s];
+            NFCS_HIP(hipMemcpyAsync(dst, c->d_arena[s], k.bytes, hipMemcpyDeviceToHost, st));
+        }
+        if (h_status)
+            NFCS_HIP(hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st));
+        NFCS_HIP(hipEventRecord(c->done[s], st));
+        i = i1;
+        s ^= 1;
+    }
+    rc = finish(s);
+    if (rc) return rc;
+    return finish(s ^ 1);
+}
+
+NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
+                                nfcs_desc* h_desc, uint64_t* arena_bytes) {
+    if (config < 0 || config > 3) return NFCS_EINVAL;
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t len = nfcs::config_len(config, seed, first_index + i);
+        if ((off >> 4) > 0xFFFFFFFFull) return NFCS_EINVAL;
+        if (h_desc) h_desc[i] = nfcs_desc{(uint32_t)(off >> 4), len};
+        off += ((uint64_t)len + 15u) & ~15ull;
+    }
+    if (arena_bytes) *arena_bytes = off;
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_gen_config_device(nfcs_ctx* c, int config, uint64_t seed, uint64_t first,
+                                    uint32_t n, uint8_t* d_arena, uint64_t arena_bytes,
+                                    const nfcs_desc* d_desc, void* stream) {
+    if (!c || config < 0 || config > 3) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!d_arena || !d_desc) return NFCS_EINVAL;
+    NFCS_HIP(nfcs::launch_gen_config(c->di, config, seed, first, n, d_arena, arena_bytes, d_desc,
+                                     pick(c, stream)));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_digest_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
+                                const nfcs_desc* d_desc, uint32_t n, uint64_t first,
+                                uint64_t* h_digest, void* stream) {
+    if (!c || !h_digest) return NFCS_EINVAL;
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipMemsetAsync(c->d_digest, 0, sizeof(uint64_t), st));
+    if (n) {
+        if (!d_arena || !d_desc) return NFCS_EINVAL;
+        NFCS_HIP(nfcs::launch_digest(c->di, d_arena, arena_bytes, d_desc, n, first, c->d_digest, st));
+    }
+    NFCS_HIP(hipMemcpyAsync(h_digest, c->d_digest, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    NFCS_HIP(hipStreamSynchronize(st));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_device_alloc(nfcs_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return NFCS_EINVAL;
+    NFCS_HIP(hipSetDevice(c->di.device));
+    hipError_t e = hipMalloc(out, bytes ? bytes : 16);
+    if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return NFCS_ENOMEM; }
+    NFCS_HIP(e);
+    return NFCS_OK;
+}
+NFCS_API int nfcs_device_free(nfcs_ctx* c, void* p) {
+    if (!c) return NFCS_EINVAL;
+    NFCS_HIP(hipFree(p));
+    return NFCS_OK;
+}
+NFCS_API int nfcs_host_alloc(nfcs_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return NFCS_EINVAL;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault);
+    if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return NFCS_ENOMEM; }
+    NFCS_HIP(e);
+    return NFCS_OK;
+}
+NFCS_API int nfcs_host_free(nfcs_ctx* c, void* p) {
+    if (!c) return NFCS_EINVAL;
+    NFCS_HIP(hipHostFree(p));
+    return NFCS_OK;
+}
+NFCS_API int nfcs_memcpy_h2d(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return NFCS_EINVAL;
+    NFCS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    NFCS_HIP(hipStreamSynchronize(c->stream));
+    return NFCS_OK;
+}
+NFCS_API int nfcs_memcpy_d2h(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return NFCS_EINVAL;
+    NFCS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    NFCS_HIP(hipStreamSynchronize(c->stream));
+    return NFCS_OK;
+}
+NFCS_API int nfcs_stream_sync(nfcs_ctx* c, void* stream) {
+    if (!c) return NFCS_EINVAL;
+    NFCS_HIP(hipStreamSynchronize(pick(c, stream)));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                     const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
+                                     int iters, void* stream, float* ms) {
+    if (!c || !ms || iters <= 0) return NFCS_EINVAL;
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it)
+        NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,
+                                     st, c->variant, c->grid));
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// nfcs_internal.h — shared between the HIP kernels (nfcs_kernels.hip) and the C-ABI /
+// context code (nfcs_api.hip). Not installed; the public boundary is include/nfcs.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nfcs.h"
+
+namespace nfcs {
+
+// Launch geometry of the checksum kernel: 256-thread blocks = 4 waves; one wave owns one
+// packet at a time (grid-stride over packets), with the next packet's first batch in flight.
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+struct LaunchCfg {
+    int grid;    // blocks
+    int variant; // kernel variant (see nfcs_kernels.hip)
+};
+
+// per-device properties cached in the context
+struct DevInfo {
+    int device = 0;
+    int cus = 256;
+    char arch[64] = {0};
+};
+
+hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
+                         const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
+                         nfcs_patch* patch, hipStream_t stream, int variant, int grid);
+
+hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint64_t first,
+                             uint32_t n, uint8_t* arena, uint64_t arena_bytes,
+                             const nfcs_desc* desc, hipStream_t stream);
+
+hipError_t launch_digest(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
+                         const nfcs_desc* desc, uint32_t n, uint64_t first, uint64_t* d_out,
+                         hipStream_t stream);
+
+// host-side synthetic layout (same spec as the device generator)
+uint32_t config_len(int config, uint64_t seed, uint64_t index);
+
+}  // namespace nfcs

@@ -1,0 +1,170 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE implementation.
+
+Run in the build container (needs /root/reference):   python tests/golden/make_golden.py
+
+It compiles the reference checksum path (header-only, include/netflow++/packet.hpp, never
+copied) through oracle/ref_shim.cpp into oracle/_ref/libnfref.so and records what the
+reference does on:
+  kat.json          the SURVEY.md Appendix-B known-answer frames (+ KAT-G/H edge cases and
+                    the reference's own tests/packet_test.cpp builder frames), full in/out hex
+  fuzz_ref.npz      N fuzz frames (oracle.nfo_fuzz_frame, seed FUZZ_SEED): per frame the
+                    length, frame_hash before and after the reference's update_checksums()
+  configs.json      digests of the synthetic configs C0..C3 before/after the
+                    reference, at full BASELINE sizes, plus per-rank shards for multi-GPU
+The fixtures are data only: frames in, frames/hashes out.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import oracle  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+FUZZ_SEED = 20250620
+FUZZ_N = 65536
+CONFIG_SEED = 20250620
+CHUNK = 1 << 16
+
+
+def be16(v):
+    return bytes([(v >> 8) & 0xFF, v & 0xFF])
+
+
+def kat_frames():
+    k = {}
+    k["A_main_cpp_tcp"] = bytes.fromhex(  # src/main.cpp:319-341
+        "0000000000aa0000000000bb0800450000281234000040060000c0a80101c0a8010a"
+        "3039005000000000000000005000000000000000")
+    k["B_packet_test_udp"] = bytes.fromhex(
+        "aabbccddeeff0011223344550800450000200001000040110000c0a8010ac0a80114d4310035000c000044415441")
+    k["C_packet_test_tcp"] = bytes.fromhex(
+        "aabbccddeeff0011223344550800450000280001000040060000c0a8010ac0a801143039005000000000"
+        "000000000000000050000000" "54455354")
+    k["D_icmp_odd"] = bytes.fromhex(
+        "00000000000000000000000008004500001d000000004001000000000000000000000800000000000000ab")
+    k["E_udp_odd_ABC"] = bytes.fromhex(
+        "aabbccddeeff00112233445508004500001f00010000401100000a0000010a00000204d2162e000b0000414243")
+    k["F_vlan_udp"] = bytes.fromhex(
+        "aabbccddeeff0011223344558100a0650800450000200001000040110000c0a8010ac0a80114d4310035000c000044415441")
+    # G: UDP whose sum folds to 0xFFFF -> checksum 0 -> stored 0xFFFF (packet.hpp:867-871)
+    eth = bytes(12) + b"\x08\x00"
+    ip = bytes([0x45, 0]) + be16(30) + bytes(4) + bytes([64, 17]) + bytes(2) + bytes([10, 0, 0, 1, 10, 0, 0, 2])
+    udp_wo = be16(4660) + be16(53) + be16(10) + bytes(2)
+    s = 0x0A00 + 0x0001 + 0x0A00 + 0x0002 + 17 + 10
+    s += 4660 + 53 + 10
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    w = 0xFFFF - s
+    k["G_udp_zero_to_ffff"] = eth + ip + udp_wo + be16(w)
+    # H: ICMP all-zero 8-byte message (exact zero sum -> 0xFFFF) and the 0xFFFF-sum twin (-> 0)
+    iph = bytes([0x45, 0]) + be16(28) + bytes(4) + bytes([64, 1]) + bytes(2) + bytes([10, 0, 0, 1, 10, 0, 0, 2])
+    k["H1_icmp_all_zero"] = eth + iph + bytes(8)
+    k["H2_icmp_sum_ffff"] = eth + iph + bytes(4) + b"\xff\xff" + bytes(2)
+    # reference test builder frames (tests/packet_test.cpp:82-138, 140-176)
+    k["I_ipv6_udp_data"] = bytes.fromhex(
+        "aabbccddeeff001122334455" "86dd" "60000000000c1140"
+        "20010db885a3000000008a2e03707334" "20010db885a3000000008a2e03707335"
+        "d4310035000c0000" "44415441")
+    k["J_ipv6_vlan_tcp"] = bytes.fromhex(
+        "aabbccddeeff001122334455" "8100a065" "86dd" "600000000018063f"
+        "20010db885a3000000008a2e03707334" "20010db885a3000000008a2e03707335"
+        "30390050000000010000000250180100abcd0000" "74657374")
+    k["K_ipv4_ihl7_tcp"] = bytes.fromhex(
+        "aabbccddeeff001122334455" "0800" "4700003500010000400600000a0000010a000002" "0102030405060708"
+        "303900500000000100000002601801001111000000000000" "7a")[:14 + 28 + 24 + 1]
+    k["L_short_13B"] = bytes(13)
+    k["M_ipv4_ihl2_udp_overlap"] = bytes.fromhex(
+        "aabbccddeeff001122334455" "0800" "42000020000100004011aaaa0a0000010a000002" "0004000c0000" "41424344")
+    return k
+
+
+def make_kat(R):
+    out = {}
+    for name, fr in kat_frames().items():
+        o_ref = oracle.ref_update_frame(fr)
+        o_orc, st = oracle.update_frame(fr)
+        assert o_ref == o_orc, name
+        out[name] = {"in": fr.hex(), "out": o_ref.hex(), "status": st}
+    with open(os.path.join(OUT, "kat.json"), "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print("kat.json:", len(out), "frames")
+
+
+def make_fuzz(R):
+    L = oracle.lib()
+    frames = oracle.fuzz_frames(FUZZ_SEED, 0, FUZZ_N)
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    h_in = np.zeros(FUZZ_N, dtype=np.uint64)
+    h_out = np.zeros(FUZZ_N, dtype=np.uint64)
+    st = np.zeros(FUZZ_N, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        b = np.frombuffer(f + bytes(16), dtype=np.uint8).copy()
+        h_in[i] = L.nfo_frame_hash(oracle._ptr(b), len(f))
+        _, s = oracle.update_frame(f)
+        st[i] = s
+        if (s & 0x3F) == 14:  # outside the reference's defined domain
+            h_out[i] = 0
+            continue
+        o = oracle.ref_update_frame(f)
+        ob = np.frombuffer(o + bytes(16), dtype=np.uint8).copy()
+        h_out[i] = L.nfo_frame_hash(oracle._ptr(ob), len(f))
+    np.savez_compressed(os.path.join(OUT, "fuzz_ref.npz"), seed=np.uint64(FUZZ_SEED), lens=lens,
+                        hash_in=h_in, hash_out=h_out, oracle_status=st)
+    print("fuzz_ref.npz:", FUZZ_N, "frames; statuses", np.unique(st, return_counts=True))
+
+
+def ref_config_digest(R, config, seed, first, n, nthreads=8):
+    """Digest of config packets [first, first+n) before and after the REFERENCE."""
+    din = dout = 0
+    M = (1 << 64) - 1
+    for lo in range(0, n, CHUNK):
+        m = min(CHUNK, n - lo)
+        arena, desc = oracle.gen_config(config, seed, first + lo, m)
+        din = (din + oracle.digest(arena, desc, first + lo)) & M
+        R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, m, nthreads)
+        dout = (dout + oracle.digest(arena, desc, first + lo)) & M
+    return din, dout
+
+
+def make_configs(R):
+    sizes = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
+    res = {"seed": CONFIG_SEED, "configs": {}}
+    for cfg, n in sizes.items():
+        t = time.time()
+        din, dout = ref_config_digest(R, cfg, CONFIG_SEED, 0, n)
+        _, odout, hist = oracle.config_digest(cfg, CONFIG_SEED, 0, n, 8)
+        assert odout == dout, (cfg, hex(odout), hex(dout))
+        res["configs"][str(cfg)] = {"first": 0, "n": n, "digest_in": f"{din:016x}",
+                                    "digest_out": f"{dout:016x}",
+                                    "oracle_status_hist": {str(k): v for k, v in hist.items()}}
+        print(f"config C{cfg} n={n}: in {din:016x} out {dout:016x}  ({time.time() - t:.1f}s)")
+    # multi-GPU weak-scaling shards of C1: rank r owns packets [r*2^20, (r+1)*2^20)
+    shards = []
+    for r in range(8):
+        t = time.time()
+        din, dout = ref_config_digest(R, 1, CONFIG_SEED, r << 20, 1 << 20)
+        shards.append({"rank": r, "first": r << 20, "n": 1 << 20, "digest_in": f"{din:016x}",
+                       "digest_out": f"{dout:016x}"})
+        print(f"C1 shard {r}: {dout:016x} ({time.time() - t:.1f}s)")
+    res["c1_rank_shards"] = shards
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    oracle.build(ref=True)
+    R = oracle.ref()
+    what = sys.argv[1:] or ["kat", "fuzz", "configs"]
+    if "kat" in what:
+        make_kat(R)
+    if "fuzz" in what:
+        make_fuzz(R)
+    if "configs" in what:
+        make_configs(R)
