@@ -33,8 +33,6 @@ namespace nfcs {
 
 #define DEV __device__ __forceinline__
 
-constexpr int kHdr = 96;  // header bytes staged in LDS per wave: l4 <= 78, fields <= l4+17
-
 DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
@@ -46,19 +44,48 @@ DEV uint32_t fold64(uint64_t s) {
     return (uint32_t)s;
 }
 
-// ---- LDS header accessors (wave-uniform offsets) -------------------------------------------
-DEV uint32_t h8(const uint8_t* h, uint32_t o) { return rfl(h[o]); }
-DEV uint32_t hbe16(const uint8_t* h, uint32_t o) {  // o even
-    return bswap16(rfl(*(const uint16_t*)(h + o)));
+// ---- staged chunk registers ------------------------------------------------------------------
+// A batch holds K chunks per lane: chunk cbase + lane + 64*k in slot k.
+template <int K>
+struct Batch {
+    uint4 v[K];
+};
+
+__device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
+
+// Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
+DEV uint32_t comp(const uint4& v, uint32_t j) {
+    const uint32_t m0 = 0u - (uint32_t)(j == 0), m1 = 0u - (uint32_t)(j == 1);
+    const uint32_t m2 = 0u - (uint32_t)(j == 2), m3 = 0u - (uint32_t)(j == 3);
+    return (v.x & m0) | (v.y & m1) | (v.z & m2) | (v.w & m3);
 }
-DEV uint32_t hle16(const uint8_t* h, uint32_t o) {  // o even
-    return rfl(*(const uint16_t*)(h + o));
+
+// Frame dword q (wave-uniform) from the registers of batch B whose first chunk is cbase.
+// With a compile-time q this folds to a single v_readlane_b32 into an SGPR.
+template <int K>
+DEV uint32_t batch_dw(const Batch<K>& B, uint32_t q, uint32_t cbase) {
+    const uint32_t rc = (q >> 2) - cbase;
+    const uint32_t k = rc >> 6, l = rc & 63u, j = q & 3u;
+    uint32_t x = 0;
+#pragma unroll
+    for (int s = 0; s < K; ++s) x |= comp(B.v[s], j) & (0u - (uint32_t)(k == (uint32_t)s));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
+
+// header accessors: frame bytes [0, 96) live in lanes 0..5 of slot 0 of the staged batch
+template <int K>
+struct Hdr {
+    const Batch<K>& B;
+    DEV uint32_t dw(uint32_t q) const { return batch_dw<K>(B, q, 0); }
+    DEV uint32_t b(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 3u))) & 0xFFu; }
+    DEV uint32_t le16(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 2u))) & 0xFFFFu; }  // o even
+    DEV uint32_t be16(uint32_t o) const { return bswap16(le16(o)); }
+};
 
 // ---- parse: everything update_checksums() decides, on wave-uniform values -------------------
 struct Plan {
     uint32_t st;      // NFCS_ST_* (without the overlap flag)
-    uint32_t mode;    // 0: write nothing, 1: fast path, 2: sequential path
+    uint32_t mode;    // 0: write nothing, 1: vector path, 2: sequential path
     uint32_t has_ip;  // IPv4 header checksum to write at ip_off (value ip_val, LE store)
     uint32_t ip_off, ip_val;
     uint32_t has_l4;  // L4 checksum over [rs, re) written at fs, fs+1
@@ -69,70 +96,43 @@ struct Plan {
     uint64_t sub;     // exact LE-domain bytes counted by the dword sum but not by the reference
 };
 
-DEV Plan parse(const uint8_t* h, uint32_t len) {
+DEV Plan plan_none(uint32_t st) {
     Plan P;
-    P.st = NFCS_ST_NONE; P.mode = 0; P.has_ip = 0; P.ip_off = 0; P.ip_val = 0; P.has_l4 = 0;
+    P.st = st; P.mode = 0; P.has_ip = 0; P.ip_off = 0; P.ip_val = 0; P.has_l4 = 0;
     P.rs = P.re = P.fs = 0; P.udp = 0; P.tailfix = 0; P.add = 0; P.sub = 0;
+    return P;
+}
 
-    // ethernet(), packet.hpp:405-418 (len < 14 keeps the ctor's 14, 346)
-    uint32_t l2 = 14;
-    if (len >= 14) l2 = (hbe16(h, 12) == 0x8100u) ? 18u : 14u;
-    uint32_t v4 = 0, proto = 0, ihl4 = 0, l4 = 0;
-    uint32_t b0 = (l2 + 20 <= len) ? h8(h, l2) : 0;
-    if (l2 + 20 <= len && (b0 >> 4) == 4) {  // 728-734: IPv4 by version nibble
-        v4 = 1;
-        proto = h8(h, l2 + 9);
-        ihl4 = (b0 & 15u) * 4u;
-        l4 = l2 + ihl4;
-        if (l2 + ihl4 > len) { P.st = NFCS_ST_OOB; return P; }  // ref reads past the frame
-        if (ihl4 < 20 && (proto == 6 || proto == 17 || proto == 1)) {
-            P.mode = 2;  // L4 region overlaps the IPv4 header: sequential path
-            return P;
-        }
-        // 739-740: checksum over ihl4 bytes with the field (l2+10) zeroed
-        uint32_t s = 0;
-        for (uint32_t w = 0; w < ihl4; w += 2)
-            if (w != 10) s += hle16(h, l2 + w);
-        P.has_ip = 1;
-        P.ip_off = l2 + 10;
-        P.ip_val = (~fold64(s)) & 0xFFFFu;
-        P.mode = 1;
-        P.st = NFCS_ST_V4;
-    } else {
-        // 741-765: effective EtherType after one 0x8100 tag; IPv6 needs the nibble too
-        uint32_t et = (len >= 14) ? hbe16(h, 12) : 0;
-        if (et == 0x8100u) et = (len >= 18) ? hbe16(h, 16) : 0;
-        if (et != 0x86DDu) return P;
-        if (!(l2 + 40 <= len && (h8(h, l2) >> 4) == 6)) return P;
-        proto = h8(h, l2 + 6);
-        l4 = l2 + 40;
-        P.st = NFCS_ST_V6;
-    }
+// L4 decisions of packet.hpp:773-889 for a packet whose L4 header starts at l4. Inlined at
+// call sites where l2/l4 are literals, so every header offset is a compile-time constant.
+template <int K>
+DEV Plan plan_l4(const Hdr<K>& H, Plan P, uint32_t len, uint32_t v4, uint32_t l2,
+                 uint32_t ihl4, uint32_t l4, uint32_t proto) {
     const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
-    uint32_t L = 0;
+    uint32_t L;
     if (proto == 6) {  // 773-823
-        if (l4 + 19 > len) { P.st = skip; return P; }   // sizeof(TcpHeader) == 19
-        uint32_t hl = (h8(h, l4 + 12) >> 4) * 4u;
+        if (l4 + 19 > len) { P.st = skip; return P; }  // sizeof(TcpHeader) == 19
+        const uint32_t hl = (H.b(l4 + 12) >> 4) * 4u;
         if (v4) {
-            uint32_t tl = hbe16(h, l2 + 2);
+            const uint32_t tl = H.be16(l2 + 2);
             if (tl < ihl4) { P.st = skip; return P; }
             L = (tl - ihl4) & 0xFFFFu;
         } else {
-            L = hbe16(h, l2 + 4);
+            L = H.be16(l2 + 4);
         }
         if (L < hl || l4 + L > len) { P.st = skip; return P; }
-        P.fs = l4 + 15;  // TcpHeader::checksum at offset 15 under #pragma pack(1)
+        P.fs = l4 + 15;  // TcpHeader::checksum sits at offset 15 under #pragma pack(1)
         P.st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
     } else if (proto == 17) {  // 824-872
         if (l4 + 8 > len) { P.st = skip; return P; }
-        L = hbe16(h, l4 + 4);
+        L = H.be16(l4 + 4);
         if (L < 8 || l4 + L > len) { P.st = skip; return P; }
         P.fs = l4 + 6;
         P.udp = 1;
         P.st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
     } else if (proto == 1 && v4) {  // 873-889
         if (l4 + 8 > len) { P.st = skip; return P; }
-        uint32_t tl = hbe16(h, l2 + 2);
+        const uint32_t tl = H.be16(l2 + 2);
         if (tl < ihl4) { P.st = skip; return P; }
         L = tl - ihl4;
         if (l4 + L > len || L < 8) { P.st = skip; return P; }
@@ -146,31 +146,75 @@ DEV Plan parse(const uint8_t* h, uint32_t len) {
     P.rs = l4;
     P.re = l4 + L;
     // pseudo-header (797-816 / 840-859) in the LE domain: address words + bswap16(proto word)
-    // + bswap16(length word). IPv6's 32-bit length has a zero upper word (L <= 0xFFFF).
-    uint64_t add = bswap16(proto) + bswap16(L);
+    // + bswap16(length word); IPv6's 32-bit length has a zero upper word (L <= 0xFFFF).
+    uint64_t add = 0;
     if (proto != 1) {
+        add = bswap16(proto) + bswap16(L);
         if (v4) {
-            for (uint32_t w = 0; w < 8; w += 2) add += hle16(h, l2 + 12 + w);
+#pragma unroll
+            for (uint32_t w = 0; w < 8; w += 2) add += H.le16(l2 + 12 + w);
         } else {
-            for (uint32_t w = 0; w < 32; w += 2) add += hle16(h, l2 + 8 + w);
+#pragma unroll
+            for (uint32_t w = 0; w < 32; w += 2) add += H.le16(l2 + 8 + w);
         }
-    } else {
-        add = 0;  // ICMP: no pseudo-header
     }
     P.add = add;
-    // Exact corrections of the dword sum: the vector pass starts at rs & ~3 (l4 is even,
-    // so it may include the two bytes rs-2, rs-1 = one LE word), and it includes the raw
-    // checksum field bytes that the reference zeroed first (795 / 838 / 885).
-    uint64_t sub = 0;
-    if (P.rs & 2u) sub += hle16(h, P.rs - 2);
-    for (uint32_t b = P.fs; b < P.fs + 2; ++b)
-        if (b >= P.rs && b < P.re) sub += (uint64_t)h8(h, b) << ((b & 1u) ? 8 : 0);
+    // exact corrections of the dword sum: the region is summed from rs & ~3 (l4 is even, so
+    // that may add the LE word at rs-2) and it includes the raw checksum field bytes that the
+    // reference zeroes before summing (795 / 838 / 885)
+    uint64_t sub = (P.rs & 2u) ? H.le16(P.rs - 2) : 0u;
+    if (P.fs >= P.rs && P.fs < P.re) sub += (uint64_t)H.b(P.fs) << ((P.fs & 1u) ? 8 : 0);
+    if (P.fs + 1 >= P.rs && P.fs + 1 < P.re) sub += (uint64_t)H.b(P.fs + 1) << (((P.fs + 1) & 1u) ? 8 : 0);
     P.sub = sub;
-    // odd region: the trailing byte (at an even frame offset, so the LOW byte of its LE word
-    // in the dword sum) must count as the HIGH byte: +255*b, unless it is a zeroed field byte
-    uint32_t t = P.re - 1;
+    // odd region: its trailing byte (even frame offset: the LOW byte of its LE word in the
+    // dword sum) counts as the HIGH byte in the reference (903-905): +255*b, unless zeroed
+    const uint32_t t = P.re - 1;
     P.tailfix = (L & 1u) && !(t >= P.fs && t < P.fs + 2);
     return P;
+}
+
+template <int K>
+DEV Plan plan_v4(const Hdr<K>& H, uint32_t len, uint32_t l2, uint32_t ihl4, uint32_t proto) {
+    Plan P = plan_none(NFCS_ST_V4);
+    // 739-740: checksum over ihl4 bytes with the field at l2+10 zeroed
+    uint64_t s = 0;
+    for (uint32_t w = 0; w < ihl4; w += 2)
+        if (w != 10) s += H.le16(l2 + w);
+    P.has_ip = 1;
+    P.ip_off = l2 + 10;
+    P.ip_val = (~fold64(s)) & 0xFFFFu;
+    P.mode = 1;
+    return plan_l4<K>(H, P, len, 1u, l2, ihl4, l2 + ihl4, proto);
+}
+
+template <int K>
+DEV Plan plan_at(const Hdr<K>& H, uint32_t len, uint32_t l2) {
+    const uint32_t b0 = (l2 + 20 <= len) ? H.b(l2) : 0u;
+    if (l2 + 20 <= len && (b0 >> 4) == 4) {  // 728-734: IPv4 by version nibble
+        const uint32_t proto = H.b(l2 + 9);
+        const uint32_t ihl4 = (b0 & 15u) * 4u;
+        if (l2 + ihl4 > len) return plan_none(NFCS_ST_OOB);  // ref reads past the frame
+        if (ihl4 < 20 && (proto == 6 || proto == 17 || proto == 1)) {
+            Plan P = plan_none(NFCS_ST_NONE);
+            P.mode = 2;  // the L4 region overlaps the IPv4 header: sequential path
+            return P;
+        }
+        if (ihl4 == 20) return plan_v4<K>(H, len, l2, 20u, proto);  // constant offsets
+        return plan_v4<K>(H, len, l2, ihl4, proto);                 // IP options
+    }
+    // 741-765: effective EtherType after one 0x8100 tag; IPv6 needs the nibble too
+    uint32_t et = (len >= 14) ? H.be16(12) : 0u;
+    if (et == 0x8100u) et = (len >= 18) ? H.be16(16) : 0u;
+    if (et != 0x86DDu || !(l2 + 40 <= len && (H.b(l2) >> 4) == 6)) return plan_none(NFCS_ST_NONE);
+    Plan P = plan_none(NFCS_ST_V6);
+    return plan_l4<K>(H, P, len, 0u, l2, 0u, l2 + 40, H.b(l2 + 6));
+}
+
+template <int K>
+DEV Plan parse(const Hdr<K>& H, uint32_t len) {
+    // ethernet(), packet.hpp:405-418: l2 = 18 after a 0x8100 tag (len < 14 keeps the ctor's 14)
+    const bool tagged = (len >= 14) && H.be16(12) == 0x8100u;
+    return tagged ? plan_at<K>(H, len, 18u) : plan_at<K>(H, len, 14u);
 }
 
 // ---- exact sequential path (IHL < 5 overlap cases), one lane --------------------------------
@@ -266,35 +310,24 @@ __device__ __noinline__ SeqOut seq_update(uint8_t* f, uint32_t len) {
     return o;
 }
 
-// ---- vector pass ----------------------------------------------------------------------------
-DEV uint32_t lowmask(int n) {  // bytes [0, n) of a dword, n clamped to [0, 4]
-    n = n < 0 ? 0 : (n > 4 ? 4 : n);
-    return n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
-}
-DEV uint32_t comp(const uint4& v, uint32_t j) {
-    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+// ---- region accumulation ---------------------------------------------------------------------
+// The L4 region [rs, re) is summed as LE dwords starting at lo4 = rs & ~3, in three parts:
+//   head: dwords in [lo4, min(lo16, re))   scalar, from the header registers (lo16 <= 80)
+//   body: full chunks in [lo16, hi16)      vector, unmasked uint4 adds into a u64 per lane
+//   tail: dwords in [hi16, re) if hi16 >= lo16: scalar, readlane of the last partial chunk
+// with lo16 = round_up(lo4, 16), hi16 = round_down(re, 16). The odd trailing byte is in the
+// head or the tail (re is odd, so never 16-aligned), where it gets its +255*b.
+DEV uint64_t masked_dw(uint32_t d, uint32_t q, uint32_t re, uint32_t tailfix) {
+    const int n = (int)re - (int)(4u * q);
+    const uint32_t m = n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : ((1u << (8 * n)) - 1u));
+    uint64_t a = d & m;
+    const uint32_t t = re - 1;
+    if (tailfix && (t >> 2) == q) a += 255ull * ((d >> (8 * (t & 3u))) & 0xFFu);
+    return a;
 }
 
-// Add chunk (16 bytes at frame offset o) restricted to dwords from lo4 (4-aligned) up to
-// byte re, plus the odd-tail fix.
-DEV void acc_chunk(uint64_t& acc, const uint4& v, uint32_t o, uint32_t lo4, uint32_t re,
-                   uint32_t tailfix) {
-    if (o >= re) return;
-    if (o >= lo4 && o + 16 <= re) {
-        acc += (uint64_t)v.x + v.y + (uint64_t)v.z + v.w;
-    } else {
-        uint64_t a = 0;
-        a += (o + 0 >= lo4) ? (v.x & lowmask((int)re - (int)(o + 0))) : 0u;
-        a += (o + 4 >= lo4) ? (v.y & lowmask((int)re - (int)(o + 4))) : 0u;
-        a += (o + 8 >= lo4) ? (v.z & lowmask((int)re - (int)(o + 8))) : 0u;
-        a += (o + 12 >= lo4) ? (v.w & lowmask((int)re - (int)(o + 12))) : 0u;
-        uint32_t t = re - 1;
-        if (tailfix && t >= o && t < o + 16) {
-            uint32_t d = comp(v, (t - o) >> 2);
-            a += 255u * ((d >> (8 * (t & 3u))) & 0xFFu);
-        }
-        acc += a;
-    }
+DEV uint64_t add_chunk(const uint4& v) {
+    return ((uint64_t)v.x + v.y) + ((uint64_t)v.z + v.w);
 }
 
 DEV uint64_t wave_sum64(uint64_t x) {
@@ -320,11 +353,6 @@ DEV uint64_t wave_sum64(uint64_t x) {
     return s;
 }
 
-template <int K>
-struct Batch {
-    uint4 v[K];
-};
-
 // One packet's staged state: descriptor and its first batch of K0 chunks per lane.
 template <int K0>
 struct Staged {
@@ -334,10 +362,13 @@ struct Staged {
     Batch<K0> b;
 };
 
+// Issue the loads of packet p's first K0*64 chunks. Every lane always issues every load
+// (lanes past the frame read g_zero16), so the number of loads in flight is the same on
+// every path and the compiler can wait with a counted vmcnt instead of vmcnt(0).
 template <int K0>
 DEV void stage(Staged<K0>& S, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                const nfcs_desc* __restrict__ desc, uint32_t p, uint32_t base16, uint32_t lane) {
-    const nfcs_desc d = desc[p];  // uniform -> s_load_dwordx2
+    const nfcs_desc d = desc[p];  // wave-uniform -> s_load_dwordx2
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     S.off = off;
     S.len = d.len;
@@ -347,12 +378,13 @@ DEV void stage(Staged<K0>& S, const uint8_t* __restrict__ arena, uint64_t arena_
 #pragma unroll
     for (int k = 0; k < K0; ++k) {
         const uint32_t c = lane + 64u * k;
-        S.b.v[k] = (c < nch) ? src[c] : make_uint4(0, 0, 0, 0);
+        const uint4* a = (c < nch) ? src + c : &g_zero16;
+        S.b.v[k] = *a;
     }
 }
 
 template <int K0, int K1>
-DEV void process(const Staged<K0>& S, uint8_t* arena, uint32_t p, uint32_t lane, uint8_t* hdr,
+DEV void process(const Staged<K0>& S, uint8_t* arena, uint32_t p, uint32_t lane,
                  uint8_t* status, nfcs_patch* patch) {
     uint32_t st;
     uint32_t ip_off = NFCS_PATCH_NONE, ip_val = 0, l4_off = NFCS_PATCH_NONE, l4_val = 0;
@@ -360,11 +392,8 @@ DEV void process(const Staged<K0>& S, uint8_t* arena, uint32_t p, uint32_t lane,
     if (S.bad) {
         st = NFCS_ST_BAD_DESC;
     } else {
-        // header bytes [0, 96) from lanes 0..5 into this wave's LDS slot
-        if (lane < kHdr / 16) ((uint4*)hdr)[lane] = S.b.v[0];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const Plan P = parse(hdr, S.len);
+        const Hdr<K0> H{S.b};
+        const Plan P = parse<K0>(H, S.len);
         st = P.st;
         if (P.mode == 2) {
             SeqOut o = {0, 0, 0, 0, 0};
@@ -374,32 +403,47 @@ DEV void process(const Staged<K0>& S, uint8_t* arena, uint32_t p, uint32_t lane,
             l4_off = rfl(o.l4_off); l4_val = rfl(o.l4_val);
         } else if (P.mode == 1) {
             if (P.has_l4) {
-                const uint32_t lo4 = P.rs & ~3u, re = P.re;
-                const uint32_t nre = (re + 15u) >> 4;  // chunks that hold region bytes
+                const uint32_t re = P.re, lo4 = P.rs & ~3u;
+                const uint32_t lo16 = (lo4 + 15u) & ~15u, hi16 = re & ~15u;
+                const uint32_t c_lo = lo16 >> 4, c_hi = hi16 >> 4;  // body chunks [c_lo, c_hi)
+                const uint32_t nre = (re + 15u) >> 4;
+                const bool has_tail = (re & 15u) && hi16 >= lo16;  // partial chunk c_hi
+                // head, scalar
+                uint64_t sc = 0;
+                const uint32_t hend = lo16 < re ? lo16 : re;
+                for (uint32_t q = lo4 >> 2; 4u * q < hend; ++q)
+                    sc += masked_dw(H.dw(q), q, re, P.tailfix);
+                // body of the staged batch, vector
                 uint64_t acc = 0;
 #pragma unroll
                 for (int k = 0; k < K0; ++k) {
                     const uint32_t c = lane + 64u * k;
-                    if (64u * k < nre) acc_chunk(acc, S.b.v[k], c * 16u, lo4, re, P.tailfix);
+                    if (c >= c_lo && c < c_hi) acc += add_chunk(S.b.v[k]);
                 }
-                // continuation batches (jumbo frames): K1 chunks per lane each
+                if (has_tail && c_hi < 64u * K0)
+                    for (uint32_t q = hi16 >> 2; 4u * q < re; ++q)
+                        sc += masked_dw(batch_dw<K0>(S.b, q, 0), q, re, P.tailfix);
+                // continuation batches (frames longer than 64*K0 chunks)
                 const uint4* src = (const uint4*)frame;
                 for (uint32_t cb = 64u * K0; cb < nre; cb += 64u * K1) {
                     Batch<K1> B;
 #pragma unroll
                     for (int k = 0; k < K1; ++k) {
                         const uint32_t c = cb + lane + 64u * k;
-                        B.v[k] = (c < nre) ? src[c] : make_uint4(0, 0, 0, 0);
+                        B.v[k] = *((c < nre) ? src + c : &g_zero16);
                     }
 #pragma unroll
                     for (int k = 0; k < K1; ++k) {
                         const uint32_t c = cb + lane + 64u * k;
-                        acc_chunk(acc, B.v[k], c * 16u, lo4, re, P.tailfix);
+                        if (c >= c_lo && c < c_hi) acc += add_chunk(B.v[k]);
                     }
+                    if (has_tail && c_hi >= cb && c_hi < cb + 64u * K1)
+                        for (uint32_t q = hi16 >> 2; 4u * q < re; ++q)
+                            sc += masked_dw(batch_dw<K1>(B, q, cb), q, re, P.tailfix);
                 }
-                const uint64_t z = wave_sum64(acc) - P.sub + P.add;
+                const uint64_t z = wave_sum64(acc) + sc + P.add - P.sub;
                 uint32_t c = (~fold64(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
-                if (P.udp && c == 0) c = 0xFFFFu;
+                if (P.udp && c == 0) c = 0xFFFFu;     // 867-871
                 l4_off = P.fs;
                 l4_val = c;
             }
@@ -435,21 +479,19 @@ __global__ __launch_bounds__(kBlock) void update_kernel(uint8_t* __restrict__ ar
                                                         uint32_t n, uint32_t base16,
                                                         uint8_t* __restrict__ status,
                                                         nfcs_patch* __restrict__ patch) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWavesPerBlock][kHdr];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wib = rfl(threadIdx.x >> 6);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    uint32_t p = blockIdx.x * kWavesPerBlock + wib;
+    uint32_t p = blockIdx.x * kWavesPerBlock + rfl(threadIdx.x >> 6);
     if (p >= n) return;
-    uint8_t* hdr = s_hdr[wib];
     Staged<K0> A;
     stage<K0>(A, arena, arena_bytes, desc, p, base16, lane);
     for (;;) {
         const uint32_t pn = p + nw;
         const bool more = pn < n && pn > p;
+        // always issue the next batch (re-read p at the end) so the wait count is static
         Staged<K0> B;
-        if (more) stage<K0>(B, arena, arena_bytes, desc, pn, base16, lane);
-        process<K0, K1>(A, arena, p, lane, hdr, status, patch);
+        stage<K0>(B, arena, arena_bytes, desc, more ? pn : p, base16, lane);
+        process<K0, K1>(A, arena, p, lane, status, patch);
         if (!more) break;
         A = B;
         p = pn;

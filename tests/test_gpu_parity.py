@@ -76,9 +76,9 @@ def test_fuzz_vs_oracle_fresh_seeds(engine, seed):
     for i, d in enumerate(desc):
         o = int(d["off16"]) * 16
         if pt[i]["ip_off"] != 0xFFFF:
-            re[o + pt[i]["ip_off"]: o + pt[i]["ip_off"] + 2] = pt[i]["ip"]
+            re[o + int(pt[i]["ip_off"]): o + int(pt[i]["ip_off"]) + 2] = pt[i]["ip"]
         if pt[i]["l4_off"] != 0xFFFF:
-            re[o + pt[i]["l4_off"]: o + pt[i]["l4_off"] + 2] = pt[i]["l4"]
+            re[o + int(pt[i]["l4_off"]): o + int(pt[i]["l4_off"]) + 2] = pt[i]["l4"]
     assert np.array_equal(re, ref)
 
 
