@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, choices=[0, 1, 2, 3])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config size)")
+    ap.add_argument("--align", type=int, default=16, help="frame start alignment in the arena (16 or 64)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -179,7 +180,7 @@ def main():
     first, n = shard(rank, n)
 
     eng = nf.Engine(local)
-    d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n)
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n, args.align)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
 
@@ -226,7 +227,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u16 one's-complement (u8 frames, u64 accumulate)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
-        "config": {"workload": WORKLOAD[args.config], "packets_per_gpu": n,
+        "config": {"workload": WORKLOAD[args.config], "packets_per_gpu": n, "frame_align": args.align,
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -138,11 +138,12 @@ NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_by
 
 /* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
 
-/* Lay out n frames of a config (packet indices first_index .. first_index+n-1) with
- * 16-byte aligned starts; fills h_desc (may be NULL) and returns the arena bytes needed
- * through *arena_bytes. Pure host code. */
+/* Lay out n frames of a config (packet indices first_index .. first_index+n-1), frame starts
+ * aligned to `align` bytes (a multiple of 16: 16 packs frames densely, 64 matches NIC
+ * buffer rings); fills h_desc (may be NULL) and returns the arena bytes needed through
+ * *arena_bytes. Pure host code. */
 NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
-                                nfcs_desc* h_desc, uint64_t* arena_bytes);
+                                uint32_t align, nfcs_desc* h_desc, uint64_t* arena_bytes);
 
 /* Fill the frames of a laid-out config batch on the device (d_desc from nfcs_layout_config). */
 NFCS_API int nfcs_gen_config_device(nfcs_ctx* ctx, int config, uint64_t seed,

@@ -17,7 +17,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libnfcs.so")
+LIB_PATH = os.environ.get("NFCS_LIB") or os.path.join(HERE, "libnfcs.so")
 HEADER = os.path.join(ROOT, "include", "nfcs.h")
 SOURCES = [os.path.join(HERE, "csrc", "nfcs_kernels.hip"), os.path.join(HERE, "csrc", "nfcs_api.hip")]
 
@@ -37,15 +37,18 @@ class NfcsError(RuntimeError):
     pass
 
 
-def build(verbose: bool = False) -> str:
-    """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree)."""
+def build(verbose: bool = False, experiments: bool = False) -> str:
+    """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree).
+    experiments=True builds netflow_amd/libnfcs_exp.so with the measurement-only ablation
+    variants (NFCS_VARIANT >= 100); the product never loads it unless NFCS_LIB points at it."""
+    out = os.path.join(HERE, "libnfcs_exp.so") if experiments else os.path.join(HERE, "libnfcs.so")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"),
-           *SOURCES, "-o", LIB_PATH]
+           *(["-DNFCS_EXPERIMENTS"] if experiments else []), *SOURCES, "-o", out]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    return LIB_PATH
+    return out
 
 
 _lib = None
@@ -64,7 +67,7 @@ def _declare(L):
         "nfcs_ctx_stream": ([_vp], _vp),
         "nfcs_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
-        "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
+        "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
         "nfcs_gen_config_device": ([_vp, ctypes.c_int, _u64, _u64, _u32, _vp, _u64, _vp, _vp], ctypes.c_int),
         "nfcs_digest_device": ([_vp, _vp, _u64, _vp, _u32, _u64, ctypes.POINTER(_u64), _vp], ctypes.c_int),
         "nfcs_device_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -103,11 +106,11 @@ def _check(rc: int, what: str):
         raise NfcsError(f"{what}: {L.nfcs_strerror(rc).decode()} (rc={rc}, hip={L.nfcs_last_hip_error()})")
 
 
-def layout_config(config: int, seed: int, first: int, n: int):
-    """Descriptors of n synthetic frames of `config` (16-byte aligned, arena order)."""
+def layout_config(config: int, seed: int, first: int, n: int, align: int = 16):
+    """Descriptors of n synthetic frames of `config` (`align`-byte aligned, arena order)."""
     desc = np.zeros(n, dtype=DESC_DTYPE)
     nbytes = _u64()
-    _check(lib().nfcs_layout_config(config, seed, first, n, desc.ctypes.data if n else None,
+    _check(lib().nfcs_layout_config(config, seed, first, n, align, desc.ctypes.data if n else None,
                                     ctypes.byref(nbytes)), "nfcs_layout_config")
     return desc, int(nbytes.value)
 
@@ -220,9 +223,9 @@ class Engine:
                                         ctypes.byref(out), stream), "digest_device")
         return int(out.value)
 
-    def config_batch(self, config: int, seed: int, first: int, n: int):
+    def config_batch(self, config: int, seed: int, first: int, n: int, align: int = 16):
         """Lay out + generate a synthetic batch on the device. Returns (arena, nbytes, desc, host_desc)."""
-        hdesc, nbytes = layout_config(config, seed, first, n)
+        hdesc, nbytes = layout_config(config, seed, first, n, align)
         d_desc = self.alloc(max(hdesc.nbytes, 16)).upload(hdesc)
         d_arena = self.alloc(max(nbytes, 16))
         self.gen_config_device(config, seed, first, n, d_arena, nbytes, d_desc)

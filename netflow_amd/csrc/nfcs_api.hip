@@ -34,11 +34,24 @@ struct nfcs_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int variant = 0;
     int grid = 0;
+    nfcs_patch* ws = nullptr;  // split-mode patch workspace (grown on demand)
+    size_t ws_cap = 0;         // records
 };
 
 namespace {
 
 thread_local int g_last_hip = 0;
+
+hipError_t ensure_ws(nfcs_ctx* c, size_t n) {
+    if (!nfcs::variant_needs_ws(c->variant) || n <= c->ws_cap) return hipSuccess;
+    if (c->ws) (void)hipFree(c->ws);
+    c->ws = nullptr;
+    c->ws_cap = 0;
+    size_t cap = n < (1u << 20) ? (1u << 20) : n;
+    hipError_t e = hipMalloc(&c->ws, cap * sizeof(nfcs_patch));
+    if (e == hipSuccess) c->ws_cap = cap;
+    return e;
+}
 
 int hip_fail(hipError_t e) {
     g_last_hip = (int)e;
@@ -154,6 +167,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
         if (c->h_patch[s]) (void)hipHostFree(c->h_patch[s]);
     }
     if (c->d_digest) (void)hipFree(c->d_digest);
+    if (c->ws) (void)hipFree(c->ws);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -169,8 +183,9 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
     if (!c) return NFCS_EINVAL;
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
+    NFCS_HIP(ensure_ws(c, n));
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
-                                 pick(c, stream), c->variant, c->grid));
+                                 pick(c, stream), c->variant, c->grid, c->ws));
     return NFCS_OK;
 }
 
@@ -250,7 +265,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         NFCS_HIP(nfcs::launch_update(c->di, c->d_arena[s], k.bytes, c->d_desc[s], m,
                                      (uint32_t)(base >> 4), c->d_status[s],
                                      patch_only ? c->d_patch[s] : nullptr, st, c->variant,
-                                     c->grid));
+                                     c->grid, c->d_patch[s]));
         if (patch_only) {
             NFCS_HIP(hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
                                     hipMemcpyDeviceToHost, st));
@@ -270,14 +285,14 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
 }
 
 NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
-                                nfcs_desc* h_desc, uint64_t* arena_bytes) {
-    if (config < 0 || config > 3) return NFCS_EINVAL;
+                                uint32_t align, nfcs_desc* h_desc, uint64_t* arena_bytes) {
+    if (config < 0 || config > 3 || align < 16 || (align & 15u)) return NFCS_EINVAL;
     uint64_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t len = nfcs::config_len(config, seed, first_index + i);
         if ((off >> 4) > 0xFFFFFFFFull) return NFCS_EINVAL;
         if (h_desc) h_desc[i] = nfcs_desc{(uint32_t)(off >> 4), len};
-        off += ((uint64_t)len + 15u) & ~15ull;
+        off += ((uint64_t)len + align - 1) / align * align;
     }
     if (arena_bytes) *arena_bytes = off;
     return NFCS_OK;
@@ -357,10 +372,11 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
                                      int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0) return NFCS_EINVAL;
     hipStream_t st = pick(c, stream);
+    NFCS_HIP(ensure_ws(c, n));
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,
-                                     st, c->variant, c->grid));
+                                     st, c->variant, c->grid, c->ws));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

@@ -29,7 +29,11 @@ struct DevInfo {
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, hipStream_t stream, int variant, int grid);
+                         nfcs_patch* patch, hipStream_t stream, int variant, int grid,
+                         nfcs_patch* ws);
+
+// variants that stage patch records in a context workspace (split mode)
+inline bool variant_needs_ws(int variant) { return variant == 8; }
 
 hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint64_t first,
                              uint32_t n, uint8_t* arena, uint64_t arena_bytes,

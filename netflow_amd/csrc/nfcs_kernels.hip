@@ -2,31 +2,34 @@
 //
 // The hot path is NetFlow++'s Packet::update_checksums() (include/netflow++/packet.hpp:722-890)
 // with its fold Packet::calculate_checksum() (packet.hpp:894-912), applied to a batch of
-// frames in HBM. Design:
+// frames in HBM. Design (every choice below was A/B-measured, profiles/):
 //
-//  * One wave64 owns one packet at a time; waves grid-stride over the batch. The descriptor
-//    is a wave-uniform scalar load; the frame streams in as 16-byte chunks, lane l holding
-//    chunks l, l+64, ... (global_load_dwordx4, fully coalesced: 1 KiB per wave-instruction).
-//    The next packet's first batch (K0 chunks per lane = 2 KiB) is issued before the current
-//    packet is reduced, so every wave keeps a packet in flight while it computes.
-//  * The first 96 bytes of the frame (every header field the reference looks at) are copied
-//    from the chunk registers of lanes 0..5 into a per-wave LDS slot. The parse — VLAN, IPv4
-//    by version nibble, IPv6, TCP/UDP/ICMP bounds rules, the 19-byte TcpHeader's checksum at
-//    offset 15 — runs on wave-uniform values (readfirstlane -> SGPRs, scalar branches). The
-//    IPv4 header checksum and the pseudo-header sum are finished from LDS on the scalar side.
+//  * One 16-lane DPP row per packet, four packets per wave64, 16 packets per 256-thread
+//    workgroup, one workgroup per 16 packets (no grid-stride loop). Lane rl of a row loads
+//    chunks rl, rl+16, ... of its frame as 16-byte global_load_dwordx4 (a row reads 256
+//    contiguous bytes per instruction); K = 6 slots cover a 1536-byte frame in one batch,
+//    longer (jumbo) frames continue in further batches of K slots.
+//  * The descriptors of a wave's four packets are consecutive: one scalar s_load_dwordx8.
+//  * All per-packet decisions run on the VALU, so one instruction serves four packets. (A
+//    wave-per-packet kernel with the parse on SGPRs measured 364 SALU + 194 VALU instructions
+//    per 1500-byte packet and was bound by the CU's single scalar unit at 1.9 TB/s.)
+//  * Header fields reach the whole row by DPP row_newbcast at compile-time offsets: an
+//    802.1Q tag is removed once per lane (one row_shl:1 + 4 selects), and the common headers
+//    (untagged/tagged x IPv4 IHL 5 / IPv6 / non-IP) are planned at constant offsets. Anything
+//    else (IP options, IHL < 5, headers past the frame) is parsed by the row's lane 0 from
+//    memory; IHL < 5 overlaps run an exact sequential emulation of the reference.
 //  * The L4 region is summed as little-endian dwords into an exact 64-bit per-lane sum. The
 //    one's-complement sum is byte-order independent (RFC 1071 §2(B)): the LE-domain fold is
 //    bswap16 of the reference's big-endian fold, so one swap at the end replaces the
-//    reference's per-word ntohs. Chunks wholly inside the region are added unmasked; the
-//    (at most two) boundary chunks per packet are masked per dword. Bytes that the
-//    reference zeroes (the checksum field) and the 2 bytes before a region that starts at
-//    2 mod 4 are subtracted exactly on the scalar side; the odd trailing byte, which the
-//    reference adds as the LOW byte (packet.hpp:903-905), gets +255*b in its lane.
-//  * The wave sum is a DPP reduction (4 row-local steps + 4 readlanes); the final fold,
-//    complement, UDP 0->0xFFFF (packet.hpp:867-871) and the 2+2 byte stores are wave-uniform.
-//  * Packets whose L4 region overlaps the IPv4 header (IHL < 5 with TCP/UDP/ICMP) go through
-//    an exact sequential emulation on one lane (same byte order of writes as the reference).
-//  * No MFMA and no LDS staging of payload: this is an HBM-read-bound integer fold.
+//    reference's per-word ntohs. Full chunks are added unmasked; at most two boundary chunks
+//    per packet are masked. The checksum field bytes (which the reference zeroes) and the 2
+//    bytes before a region starting at 2 mod 4 are subtracted exactly; the odd trailing byte,
+//    which the reference adds as the LOW byte (packet.hpp:903-905), gets +255*b.
+//  * Row sum: four DPP steps. Final fold, complement, UDP 0 -> 0xFFFF (packet.hpp:867-871),
+//    then the 2+2 checksum bytes are stored from lanes 0..3 of the row.
+//  * Cache policy: the header slot is loaded with the default policy and the payload slots
+//    with non-temporal (evict-first) loads (measured best for the 1500-byte config).
+//  * No MFMA and no LDS staging: this is an HBM-read-bound integer fold.
 #include "nfcs_internal.h"
 
 namespace nfcs {
@@ -45,12 +48,6 @@ DEV uint32_t fold64(uint64_t s) {
 }
 
 // ---- staged chunk registers ------------------------------------------------------------------
-// A batch holds K chunks per lane: chunk cbase + lane + 64*k in slot k.
-template <int K>
-struct Batch {
-    uint4 v[K];
-};
-
 __device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
@@ -60,162 +57,6 @@ DEV uint32_t comp(const uint4& v, uint32_t j) {
     return (v.x & m0) | (v.y & m1) | (v.z & m2) | (v.w & m3);
 }
 
-// Frame dword q (wave-uniform) from the registers of batch B whose first chunk is cbase.
-// With a compile-time q this folds to a single v_readlane_b32 into an SGPR.
-template <int K>
-DEV uint32_t batch_dw(const Batch<K>& B, uint32_t q, uint32_t cbase) {
-    const uint32_t rc = (q >> 2) - cbase;
-    const uint32_t k = rc >> 6, l = rc & 63u, j = q & 3u;
-    uint32_t x = 0;
-#pragma unroll
-    for (int s = 0; s < K; ++s) x |= comp(B.v[s], j) & (0u - (uint32_t)(k == (uint32_t)s));
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
-}
-
-// header accessors: frame bytes [0, 96) live in lanes 0..5 of slot 0 of the staged batch
-template <int K>
-struct Hdr {
-    const Batch<K>& B;
-    DEV uint32_t dw(uint32_t q) const { return batch_dw<K>(B, q, 0); }
-    DEV uint32_t b(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 3u))) & 0xFFu; }
-    DEV uint32_t le16(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 2u))) & 0xFFFFu; }  // o even
-    DEV uint32_t be16(uint32_t o) const { return bswap16(le16(o)); }
-};
-
-// ---- parse: everything update_checksums() decides, on wave-uniform values -------------------
-struct Plan {
-    uint32_t st;      // NFCS_ST_* (without the overlap flag)
-    uint32_t mode;    // 0: write nothing, 1: vector path, 2: sequential path
-    uint32_t has_ip;  // IPv4 header checksum to write at ip_off (value ip_val, LE store)
-    uint32_t ip_off, ip_val;
-    uint32_t has_l4;  // L4 checksum over [rs, re) written at fs, fs+1
-    uint32_t rs, re, fs;
-    uint32_t udp;     // 0 -> 0xFFFF rule
-    uint32_t tailfix; // odd region: trailing byte counts as the low byte
-    uint64_t add;     // exact LE-domain constant: pseudo-header
-    uint64_t sub;     // exact LE-domain bytes counted by the dword sum but not by the reference
-};
-
-DEV Plan plan_none(uint32_t st) {
-    Plan P;
-    P.st = st; P.mode = 0; P.has_ip = 0; P.ip_off = 0; P.ip_val = 0; P.has_l4 = 0;
-    P.rs = P.re = P.fs = 0; P.udp = 0; P.tailfix = 0; P.add = 0; P.sub = 0;
-    return P;
-}
-
-// L4 decisions of packet.hpp:773-889 for a packet whose L4 header starts at l4. Inlined at
-// call sites where l2/l4 are literals, so every header offset is a compile-time constant.
-template <int K>
-DEV Plan plan_l4(const Hdr<K>& H, Plan P, uint32_t len, uint32_t v4, uint32_t l2,
-                 uint32_t ihl4, uint32_t l4, uint32_t proto) {
-    const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
-    uint32_t L;
-    if (proto == 6) {  // 773-823
-        if (l4 + 19 > len) { P.st = skip; return P; }  // sizeof(TcpHeader) == 19
-        const uint32_t hl = (H.b(l4 + 12) >> 4) * 4u;
-        if (v4) {
-            const uint32_t tl = H.be16(l2 + 2);
-            if (tl < ihl4) { P.st = skip; return P; }
-            L = (tl - ihl4) & 0xFFFFu;
-        } else {
-            L = H.be16(l2 + 4);
-        }
-        if (L < hl || l4 + L > len) { P.st = skip; return P; }
-        P.fs = l4 + 15;  // TcpHeader::checksum sits at offset 15 under #pragma pack(1)
-        P.st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
-    } else if (proto == 17) {  // 824-872
-        if (l4 + 8 > len) { P.st = skip; return P; }
-        L = H.be16(l4 + 4);
-        if (L < 8 || l4 + L > len) { P.st = skip; return P; }
-        P.fs = l4 + 6;
-        P.udp = 1;
-        P.st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
-    } else if (proto == 1 && v4) {  // 873-889
-        if (l4 + 8 > len) { P.st = skip; return P; }
-        const uint32_t tl = H.be16(l2 + 2);
-        if (tl < ihl4) { P.st = skip; return P; }
-        L = tl - ihl4;
-        if (l4 + L > len || L < 8) { P.st = skip; return P; }
-        P.fs = l4 + 2;
-        P.st = NFCS_ST_V4_ICMP;
-    } else {
-        return P;  // IPv4 header only (v4) / nothing (v6)
-    }
-    P.mode = 1;
-    P.has_l4 = 1;
-    P.rs = l4;
-    P.re = l4 + L;
-    // pseudo-header (797-816 / 840-859) in the LE domain: address words + bswap16(proto word)
-    // + bswap16(length word); IPv6's 32-bit length has a zero upper word (L <= 0xFFFF).
-    uint64_t add = 0;
-    if (proto != 1) {
-        add = bswap16(proto) + bswap16(L);
-        if (v4) {
-#pragma unroll
-            for (uint32_t w = 0; w < 8; w += 2) add += H.le16(l2 + 12 + w);
-        } else {
-#pragma unroll
-            for (uint32_t w = 0; w < 32; w += 2) add += H.le16(l2 + 8 + w);
-        }
-    }
-    P.add = add;
-    // exact corrections of the dword sum: the region is summed from rs & ~3 (l4 is even, so
-    // that may add the LE word at rs-2) and it includes the raw checksum field bytes that the
-    // reference zeroes before summing (795 / 838 / 885)
-    uint64_t sub = (P.rs & 2u) ? H.le16(P.rs - 2) : 0u;
-    if (P.fs >= P.rs && P.fs < P.re) sub += (uint64_t)H.b(P.fs) << ((P.fs & 1u) ? 8 : 0);
-    if (P.fs + 1 >= P.rs && P.fs + 1 < P.re) sub += (uint64_t)H.b(P.fs + 1) << (((P.fs + 1) & 1u) ? 8 : 0);
-    P.sub = sub;
-    // odd region: its trailing byte (even frame offset: the LOW byte of its LE word in the
-    // dword sum) counts as the HIGH byte in the reference (903-905): +255*b, unless zeroed
-    const uint32_t t = P.re - 1;
-    P.tailfix = (L & 1u) && !(t >= P.fs && t < P.fs + 2);
-    return P;
-}
-
-template <int K>
-DEV Plan plan_v4(const Hdr<K>& H, uint32_t len, uint32_t l2, uint32_t ihl4, uint32_t proto) {
-    Plan P = plan_none(NFCS_ST_V4);
-    // 739-740: checksum over ihl4 bytes with the field at l2+10 zeroed
-    uint64_t s = 0;
-    for (uint32_t w = 0; w < ihl4; w += 2)
-        if (w != 10) s += H.le16(l2 + w);
-    P.has_ip = 1;
-    P.ip_off = l2 + 10;
-    P.ip_val = (~fold64(s)) & 0xFFFFu;
-    P.mode = 1;
-    return plan_l4<K>(H, P, len, 1u, l2, ihl4, l2 + ihl4, proto);
-}
-
-template <int K>
-DEV Plan plan_at(const Hdr<K>& H, uint32_t len, uint32_t l2) {
-    const uint32_t b0 = (l2 + 20 <= len) ? H.b(l2) : 0u;
-    if (l2 + 20 <= len && (b0 >> 4) == 4) {  // 728-734: IPv4 by version nibble
-        const uint32_t proto = H.b(l2 + 9);
-        const uint32_t ihl4 = (b0 & 15u) * 4u;
-        if (l2 + ihl4 > len) return plan_none(NFCS_ST_OOB);  // ref reads past the frame
-        if (ihl4 < 20 && (proto == 6 || proto == 17 || proto == 1)) {
-            Plan P = plan_none(NFCS_ST_NONE);
-            P.mode = 2;  // the L4 region overlaps the IPv4 header: sequential path
-            return P;
-        }
-        if (ihl4 == 20) return plan_v4<K>(H, len, l2, 20u, proto);  // constant offsets
-        return plan_v4<K>(H, len, l2, ihl4, proto);                 // IP options
-    }
-    // 741-765: effective EtherType after one 0x8100 tag; IPv6 needs the nibble too
-    uint32_t et = (len >= 14) ? H.be16(12) : 0u;
-    if (et == 0x8100u) et = (len >= 18) ? H.be16(16) : 0u;
-    if (et != 0x86DDu || !(l2 + 40 <= len && (H.b(l2) >> 4) == 6)) return plan_none(NFCS_ST_NONE);
-    Plan P = plan_none(NFCS_ST_V6);
-    return plan_l4<K>(H, P, len, 0u, l2, 0u, l2 + 40, H.b(l2 + 6));
-}
-
-template <int K>
-DEV Plan parse(const Hdr<K>& H, uint32_t len) {
-    // ethernet(), packet.hpp:405-418: l2 = 18 after a 0x8100 tag (len < 14 keeps the ctor's 14)
-    const bool tagged = (len >= 14) && H.be16(12) == 0x8100u;
-    return tagged ? plan_at<K>(H, len, 18u) : plan_at<K>(H, len, 14u);
-}
 
 // ---- exact sequential path (IHL < 5 overlap cases), one lane --------------------------------
 // Mirrors packet.hpp:722-890 byte by byte on global memory, in the reference's write order.
@@ -330,7 +171,281 @@ DEV uint64_t add_chunk(const uint4& v) {
     return ((uint64_t)v.x + v.y) + ((uint64_t)v.z + v.w);
 }
 
-DEV uint64_t wave_sum64(uint64_t x) {
+// =============================================================================================
+// v3: one 16-lane DPP row per packet, four packets per wave, all per-packet logic on the VALU.
+//
+// v2 (one wave per packet, parse on SGPRs) measured 364 SALU + 194 VALU instructions per
+// 1500 B packet: the CU's single scalar unit, not HBM, set the rate (profiles/). Here every
+// per-packet decision runs once per 16-lane row, so one VALU instruction serves four packets
+// and the scalar unit only runs the loop. Lane rl of a row holds chunks rl, rl+16, ... of its
+// packet; header dwords reach the whole row by DPP row_newbcast (compile-time offsets) or
+// ds_bpermute (runtime offsets: IP options, IPv6); the row sum is four DPP steps.
+// =============================================================================================
+
+template <int L>
+DEV uint32_t row_bcast(uint32_t x) {  // lane L of this lane's 16-lane row
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + L, 0xF, 0xF, false);
+}
+
+// Per-lane view of the header bytes [0, 256) of the row's packet: lane rl of the row holds
+// chunk rl (frame bytes 16rl .. 16rl+15) of slot 0.
+struct RowHdr {
+    uint4 c0;
+    uint32_t rowbase4;  // byte address of lane 0 of this row, for ds_bpermute
+    DEV uint32_t dw(uint32_t q) const {
+        const uint32_t x = comp(c0, q & 3u);
+        if (__builtin_constant_p(q)) {
+            switch ((q >> 2) & 15u) {
+            case 0: return row_bcast<0>(x);   case 1: return row_bcast<1>(x);
+            case 2: return row_bcast<2>(x);   case 3: return row_bcast<3>(x);
+            case 4: return row_bcast<4>(x);   case 5: return row_bcast<5>(x);
+            case 6: return row_bcast<6>(x);   case 7: return row_bcast<7>(x);
+            case 8: return row_bcast<8>(x);   case 9: return row_bcast<9>(x);
+            case 10: return row_bcast<10>(x); case 11: return row_bcast<11>(x);
+            case 12: return row_bcast<12>(x); case 13: return row_bcast<13>(x);
+            case 14: return row_bcast<14>(x); default: return row_bcast<15>(x);
+            }
+        }
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rowbase4 + ((q >> 2) & 15u) * 4u), (int)x);
+    }
+    DEV uint32_t b(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 3u))) & 0xFFu; }
+    DEV uint32_t le16(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 2u))) & 0xFFFFu; }
+    DEV uint32_t be16(uint32_t o) const { return bswap16(le16(o)); }
+};
+
+// Compact per-lane plan (row-uniform values).
+enum : uint32_t { F_IP = 1, F_L4 = 2, F_UDP = 4, F_TAIL = 8, F_SEQ = 16 };
+struct RPlan {
+    uint32_t st;     // status byte
+    uint32_t flags;  // F_*
+    uint32_t ipw;    // ip_off | ip_val << 16
+    uint32_t rs, re, fs;
+    uint64_t corr;   // pseudo-header add minus over-counted bytes (two's complement)
+};
+
+DEV RPlan rplan_none(uint32_t st) {
+    RPlan P;
+    P.st = st; P.flags = 0; P.ipw = 0; P.rs = 0; P.re = 0; P.fs = 0; P.corr = 0;
+    return P;
+}
+
+// Header bytes with an 802.1Q tag removed: view byte o (o >= 12) is frame byte o + 4*tagged.
+// The reference's offsets are all relative to l2 = 14 or 18 (ethernet(), packet.hpp:405-418),
+// so one plan written at l2 = 14 serves both framings. Each lane shifts its own chunk by one
+// dword (the 4th dword comes from the next lane of the row via DPP row_shl:1), so every
+// header access afterwards is a single row broadcast at a compile-time offset.
+DEV uint4 strip_tag(const uint4& c, bool tagged) {
+    const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)c.x, 0x101, 0xF, 0xF, true);
+    const uint32_t m = 0u - (uint32_t)tagged;
+    return make_uint4((c.x & ~m) | (c.y & m), (c.y & ~m) | (c.z & m),
+                      (c.z & ~m) | (c.w & m), (c.w & ~m) | (nx & m));
+}
+
+using View = RowHdr;
+
+// L4 branch of packet.hpp:773-889 in view coordinates with compile-time l2 = 14 and l4
+// (34 for IPv4 with IHL 5, 54 for IPv6); sh = 4 for tagged frames shifts the frame offsets.
+DEV RPlan fast_l4(const View& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l4, uint32_t proto,
+                  uint32_t sh) {
+    const uint32_t l2 = 14, ihl4 = 20;
+    const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
+    uint32_t L, fs, st, fl = F_L4;
+    if (proto == 6) {
+        if (l4 + 19 > lenv) { P.st = skip; return P; }  // sizeof(TcpHeader) == 19
+        const uint32_t hl = (V.b(l4 + 12) >> 4) * 4u;
+        if (v4) {
+            const uint32_t tl = V.be16(l2 + 2);
+            if (tl < ihl4) { P.st = skip; return P; }
+            L = (tl - ihl4) & 0xFFFFu;
+        } else {
+            L = V.be16(l2 + 4);
+        }
+        if (L < hl || l4 + L > lenv) { P.st = skip; return P; }
+        fs = l4 + 15;  // TcpHeader::checksum at offset 15 (19-byte packed struct)
+        st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
+    } else if (proto == 17) {
+        if (l4 + 8 > lenv) { P.st = skip; return P; }
+        L = V.be16(l4 + 4);
+        if (L < 8 || l4 + L > lenv) { P.st = skip; return P; }
+        fs = l4 + 6;
+        fl |= F_UDP;
+        st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
+    } else if (proto == 1 && v4) {
+        if (l4 + 8 > lenv) { P.st = skip; return P; }
+        const uint32_t tl = V.be16(l2 + 2);
+        if (tl < ihl4) { P.st = skip; return P; }
+        L = tl - ihl4;
+        if (l4 + L > lenv || L < 8) { P.st = skip; return P; }
+        fs = l4 + 2;
+        st = NFCS_ST_V4_ICMP;
+    } else {
+        return P;
+    }
+    uint64_t add = 0;
+    if (proto != 1) {  // pseudo-header in the LE domain (797-816 / 840-859)
+        add = bswap16(proto) + bswap16(L);
+        if (v4) {
+#pragma unroll
+            for (uint32_t w = 0; w < 8; w += 2) add += V.le16(l2 + 12 + w);
+        } else {
+#pragma unroll
+            for (uint32_t w = 0; w < 32; w += 2) add += V.le16(l2 + 8 + w);
+        }
+    }
+    // over-counted bytes: the LE word before l4 when l4 = 2 mod 4 (sh keeps the parity), and
+    // the raw checksum field bytes the reference zeroes first (795 / 838 / 885)
+    const uint32_t re = l4 + L;
+    uint64_t sub = ((l4 + sh) & 2u) ? V.le16(l4 - 2) : 0u;
+    if (fs < re) sub += (uint64_t)V.b(fs) << (((fs + sh) & 1u) ? 8 : 0);
+    if (fs + 1 < re) sub += (uint64_t)V.b(fs + 1) << (((fs + 1 + sh) & 1u) ? 8 : 0);
+    const uint32_t t = re - 1;
+    if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
+    P.st = st;
+    P.flags |= fl;
+    P.rs = l4 + sh;
+    P.re = re + sh;
+    P.fs = fs + sh;
+    P.corr = add - sub;
+    return P;
+}
+
+// Common headers with compile-time offsets: untagged / 802.1Q; IPv4 with IHL 5; IPv6; non-IP.
+// Returns F_SEQ in flags for everything else (IHL != 5: options, IHL < 5, past the frame).
+DEV RPlan fast_plan(const uint4& c0, uint32_t rowbase4, uint32_t len) {
+    const RowHdr h{c0, rowbase4};
+    const bool tagged = (len >= 14) && h.be16(12) == 0x8100u;  // ethernet(): l2 = 18
+    const uint32_t sh = tagged ? 4u : 0u;
+    const View V{strip_tag(c0, tagged), rowbase4};
+    const uint32_t lenv = len - sh;  // len >= 14 whenever tagged
+    const uint32_t b0 = V.b(14);
+    if (len >= 14 + sh && lenv >= 34 && (b0 >> 4) == 4) {  // 728-734: IPv4 by nibble
+        if ((b0 & 15u) != 5) return rplan_none(NFCS_ST_NONE | (F_SEQ << 8));
+        uint64_t s = 0;  // 739-740: header checksum, field zeroed
+#pragma unroll
+        for (uint32_t w = 0; w < 20; w += 2)
+            if (w != 10) s += V.le16(14 + w);
+        RPlan P = rplan_none(NFCS_ST_V4);
+        P.flags = F_IP;
+        P.ipw = (24u + sh) | (((~fold64(s)) & 0xFFFFu) << 16);
+        return fast_l4(V, P, lenv, 1u, 34u, V.b(23), sh);
+    }
+    // 741-765: effective EtherType (after one tag) must be IPv6 and the nibble 6
+    const uint32_t et = (len >= 14 + sh) ? V.be16(12) : 0u;
+    if (et != 0x86DDu || !(len >= 14 + sh && lenv >= 54 && (b0 >> 4) == 6))
+        return rplan_none(NFCS_ST_NONE);
+    return fast_l4(V, rplan_none(NFCS_ST_V6), lenv, 0u, 54u, V.b(20), sh);
+}
+
+// Any header, parsed by one lane from global memory (IP options, IHL < 5, past the frame).
+__device__ __noinline__ RPlan slow_plan(const uint8_t* f, uint32_t len) {
+    uint32_t l2 = 14;
+    if (len >= 14) l2 = (g_be16(f, 12) == 0x8100u) ? 18u : 14u;
+    RPlan P = rplan_none(NFCS_ST_NONE);
+    uint32_t v4 = 0, proto, ihl4 = 0, l4;
+    if (l2 + 20 <= len && (f[l2] >> 4) == 4) {
+        v4 = 1;
+        proto = f[l2 + 9];
+        ihl4 = (f[l2] & 15u) * 4u;
+        l4 = l2 + ihl4;
+        if (l2 + ihl4 > len) return rplan_none(NFCS_ST_OOB);
+        if (ihl4 < 20 && (proto == 6 || proto == 17 || proto == 1)) {
+            P.flags = F_SEQ;  // overlapping headers: full sequential emulation
+            return P;
+        }
+        uint32_t s = 0;
+        for (uint32_t w = 0; w < ihl4; w += 2)
+            if (w != 10) s += g_be16(f, l2 + w);
+        P.st = NFCS_ST_V4;
+        P.flags = F_IP;
+        P.ipw = (l2 + 10) | (bswap16(g_fin(s)) << 16);
+    } else {
+        uint32_t et = (len >= 14) ? g_be16(f, 12) : 0;
+        if (et == 0x8100u) et = (len >= 18) ? g_be16(f, 16) : 0;
+        if (et != 0x86DDu || !(l2 + 40 <= len && (f[l2] >> 4) == 6)) return P;
+        proto = f[l2 + 6];
+        l4 = l2 + 40;
+        P.st = NFCS_ST_V6;
+    }
+    const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
+    uint32_t L, fs, st, fl = F_L4;
+    if (proto == 6) {
+        if (l4 + 19 > len) { P.st = skip; return P; }
+        const uint32_t hl = (f[l4 + 12] >> 4) * 4u;
+        if (v4) {
+            const uint32_t tl = g_be16(f, l2 + 2);
+            if (tl < ihl4) { P.st = skip; return P; }
+            L = (tl - ihl4) & 0xFFFFu;
+        } else {
+            L = g_be16(f, l2 + 4);
+        }
+        if (L < hl || l4 + L > len) { P.st = skip; return P; }
+        fs = l4 + 15;
+        st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
+    } else if (proto == 17) {
+        if (l4 + 8 > len) { P.st = skip; return P; }
+        L = g_be16(f, l4 + 4);
+        if (L < 8 || l4 + L > len) { P.st = skip; return P; }
+        fs = l4 + 6;
+        fl |= F_UDP;
+        st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
+    } else if (proto == 1 && v4) {
+        if (l4 + 8 > len) { P.st = skip; return P; }
+        const uint32_t tl = g_be16(f, l2 + 2);
+        if (tl < ihl4) { P.st = skip; return P; }
+        L = tl - ihl4;
+        if (l4 + L > len || L < 8) { P.st = skip; return P; }
+        fs = l4 + 2;
+        st = NFCS_ST_V4_ICMP;
+    } else {
+        return P;
+    }
+    uint64_t add = 0;
+    if (proto != 1) {
+        add = bswap16(proto) + bswap16(L);
+        const uint32_t a0 = v4 ? l2 + 12 : l2 + 8, an = v4 ? 8u : 32u;
+        for (uint32_t w = 0; w < an; w += 2) add += bswap16(g_be16(f, a0 + w));
+    }
+    const uint32_t re = l4 + L;
+    uint64_t sub = (l4 & 2u) ? bswap16(g_be16(f, l4 - 2)) : 0u;
+    if (fs < re) sub += (uint64_t)f[fs] << ((fs & 1u) ? 8 : 0);
+    if (fs + 1 < re) sub += (uint64_t)f[fs + 1] << (((fs + 1) & 1u) ? 8 : 0);
+    const uint32_t t = re - 1;
+    if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
+    P.st = st;
+    P.flags |= fl;
+    P.rs = l4;
+    P.re = re;
+    P.fs = fs;
+    P.corr = add - sub;
+    return P;
+}
+
+// Masked add of one boundary chunk at frame offset o: dwords from lo4 up to byte re, plus the
+// odd-tail fix.
+DEV uint64_t masked_chunk(const uint4& v, uint32_t o, uint32_t lo4, uint32_t re, uint32_t tailfix) {
+    uint64_t a = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t od = o + 4u * j;
+        const int nb = (int)re - (int)od;
+        uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+        m = (od >= lo4) ? m : 0u;
+        a += comp(v, j) & m;
+    }
+    const uint32_t t = re - 1;
+    if (tailfix && t >= o && t < o + 16) a += 255ull * ((comp(v, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+    return a;
+}
+
+DEV void acc_slot(uint64_t& acc, const uint4& v, uint32_t c, uint32_t lo4, uint32_t re, uint32_t tailfix) {
+    const uint32_t o = c * 16u;
+    const bool full = (o >= lo4) && (o + 16u <= re);
+    const bool part = !full && (o + 16u > lo4) && (o < re);
+    if (full) acc += add_chunk(v);
+    if (part) acc += masked_chunk(v, o, lo4, re, tailfix);
+}
+
+DEV uint64_t row_sum64(uint64_t x) {  // every lane of a 16-lane row gets the row's sum
     uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
 #define NFCS_DPP_STEP(ctrl)                                                              \
     {                                                                                    \
@@ -340,186 +455,334 @@ DEV uint64_t wave_sum64(uint64_t x) {
         lo = (uint32_t)s_;                                                               \
         hi = (uint32_t)(s_ >> 32);                                                       \
     }
-    NFCS_DPP_STEP(0xB1)   // quad_perm [1,0,3,2]
-    NFCS_DPP_STEP(0x4E)   // quad_perm [2,3,0,1]
-    NFCS_DPP_STEP(0x141)  // row_half_mirror
-    NFCS_DPP_STEP(0x140)  // row_mirror: every lane of a 16-lane row now holds the row sum
+    NFCS_DPP_STEP(0xB1)
+    NFCS_DPP_STEP(0x4E)
+    NFCS_DPP_STEP(0x141)
+    NFCS_DPP_STEP(0x140)
 #undef NFCS_DPP_STEP
-    uint64_t s = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        s += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
-    return s;
+    return ((uint64_t)hi << 32) | lo;
 }
 
-// One packet's staged state: descriptor and its first batch of K0 chunks per lane.
-template <int K0>
-struct Staged {
-    uint64_t off;  // byte offset of the frame in the arena (wave-uniform)
-    uint32_t len;
-    uint32_t bad;
-    Batch<K0> b;
+DEV uint32_t wave_max_rows(uint32_t x) {  // x row-uniform
+    uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 16));
+    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 32));
+    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
+    return m;
+}
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int NT>
+DEV uint4 ld16(const uint4* p) {
+    if (NT) {
+        const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)p);
+        return make_uint4(t.x, t.y, t.z, t.w);
+    }
+    return *p;
+}
+
+// Descriptors of the wave's four rows: packets w, w+1, w+2, w+3 are consecutive in the
+// descriptor array, so one wave-uniform scalar load (s_load_dwordx8) fetches all four; each
+// lane picks its row's pair. Counted on lgkmcnt, so prefetching them never holds up a vmcnt
+// wait for chunk data.
+struct Desc4 { uint32_t w[8]; };
+
+DEV Desc4 load_desc4(const nfcs_desc* __restrict__ desc, uint64_t pw, uint32_t n) {
+    Desc4 D;
+    if (pw + 4 <= n) {
+        const uint32_t* q = (const uint32_t*)(desc + pw);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) D.w[i] = q[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = pw + i < n;
+            D.w[2 * i] = ok ? desc[pw + i].off16 : 0u;
+            D.w[2 * i + 1] = ok ? desc[pw + i].len : 0u;
+        }
+    }
+    return D;
+}
+
+DEV nfcs_desc pick_desc(const Desc4& D, uint32_t row) {  // mask selects: no indexable temp
+    const uint32_t m0 = 0u - (uint32_t)(row == 0), m1 = 0u - (uint32_t)(row == 1);
+    const uint32_t m2 = 0u - (uint32_t)(row == 2), m3 = 0u - (uint32_t)(row == 3);
+    nfcs_desc d;
+    d.off16 = (D.w[0] & m0) | (D.w[2] & m1) | (D.w[4] & m2) | (D.w[6] & m3);
+    d.len = (D.w[1] & m0) | (D.w[3] & m1) | (D.w[5] & m2) | (D.w[7] & m3);
+    return d;
+}
+
+// One row's packet, staged: frame window and its first K slots of chunks in flight.
+template <int K>
+struct RowStage {
+    uint4 v[K];
+    uint8_t* frame;
+    uint32_t len;   // 0 unless live
+    uint32_t p;
+    uint32_t valid, bad;
 };
 
-// Issue the loads of packet p's first K0*64 chunks. Every lane always issues every load
-// (lanes past the frame read g_zero16), so the number of loads in flight is the same on
-// every path and the compiler can wait with a counted vmcnt instead of vmcnt(0).
-template <int K0>
-DEV void stage(Staged<K0>& S, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-               const nfcs_desc* __restrict__ desc, uint32_t p, uint32_t base16, uint32_t lane) {
-    const nfcs_desc d = desc[p];  // wave-uniform -> s_load_dwordx2
+template <int K, int NT>
+DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl) {
+    const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
-    S.off = off;
-    S.len = d.len;
-    S.bad = (d.off16 < base16) || (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes);
-    const uint32_t nch = S.bad ? 0u : (d.len + 15u) >> 4;
-    const uint4* src = (const uint4*)(arena + off);
+    const bool bad = valid && ((d.off16 < base16) ||
+                               (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
+    const bool live = valid && !bad;
+    S.valid = valid;
+    S.bad = bad;
+    S.p = (uint32_t)p64;
+    S.len = live ? d.len : 0u;
+    S.frame = arena + (live ? off : 0);
+    const uint32_t nch = (S.len + 15u) >> 4;
+    const uint4* src = (const uint4*)S.frame;
+    // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
 #pragma unroll
-    for (int k = 0; k < K0; ++k) {
-        const uint32_t c = lane + 64u * k;
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = rl + 16u * k;
         const uint4* a = (c < nch) ? src + c : &g_zero16;
-        S.b.v[k] = *a;
+        // NT 2: the header slot keeps the default policy so its lines are still in L2 when
+        // the checksum chunks are written back; payload slots stream through as evict-first
+        S.v[k] = (NT == 2 && k == 0) ? ld16<0>(a) : ld16<NT>(a);
     }
 }
 
-template <int K0, int K1>
-DEV void process(const Staged<K0>& S, uint8_t* arena, uint32_t p, uint32_t lane,
-                 uint8_t* status, nfcs_patch* patch) {
-    uint32_t st;
-    uint32_t ip_off = NFCS_PATCH_NONE, ip_val = 0, l4_off = NFCS_PATCH_NONE, l4_val = 0;
-    uint8_t* frame = arena + S.off;
-    if (S.bad) {
-        st = NFCS_ST_BAD_DESC;
+// DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
+// (no parse), 3 = both.
+template <int K, int NT, int DBG = 0, int SM = 0>
+DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
+                     nfcs_patch* patch) {
+    const uint32_t len = S.len;
+    uint8_t* frame = S.frame;
+    const uint4* src = (const uint4*)frame;
+    RPlan P;
+    if (DBG & 2) {
+        P = rplan_none(NFCS_ST_V4_UDP);
+        P.flags = F_IP | F_L4 | F_UDP; P.ipw = 24; P.rs = 34; P.re = len; P.fs = 40; P.corr = 0;
     } else {
-        const Hdr<K0> H{S.b};
-        const Plan P = parse<K0>(H, S.len);
-        st = P.st;
-        if (P.mode == 2) {
-            SeqOut o = {0, 0, 0, 0, 0};
-            if (lane == 0) o = seq_update(frame, S.len);
-            st = rfl(o.st) | NFCS_ST_FLAG_OVERLAP;
-            ip_off = rfl(o.ip_off); ip_val = rfl(o.ip_val);
-            l4_off = rfl(o.l4_off); l4_val = rfl(o.l4_val);
-        } else if (P.mode == 1) {
-            if (P.has_l4) {
-                const uint32_t re = P.re, lo4 = P.rs & ~3u;
-                const uint32_t lo16 = (lo4 + 15u) & ~15u, hi16 = re & ~15u;
-                const uint32_t c_lo = lo16 >> 4, c_hi = hi16 >> 4;  // body chunks [c_lo, c_hi)
-                const uint32_t nre = (re + 15u) >> 4;
-                const bool has_tail = (re & 15u) && hi16 >= lo16;  // partial chunk c_hi
-                // head, scalar
-                uint64_t sc = 0;
-                const uint32_t hend = lo16 < re ? lo16 : re;
-                for (uint32_t q = lo4 >> 2; 4u * q < hend; ++q)
-                    sc += masked_dw(H.dw(q), q, re, P.tailfix);
-                // body of the staged batch, vector
-                uint64_t acc = 0;
+        P = fast_plan(S.v[0], rowbase4, len);
+    }
+    if (P.st >> 8) {  // uncommon header: parsed by the row's lane 0, broadcast to the row
+        RPlan Q = rplan_none(0);
+        if (rl == 0) Q = slow_plan(frame, len);
+        P.st = row_bcast<0>(Q.st);
+        P.flags = row_bcast<0>(Q.flags);
+        P.ipw = row_bcast<0>(Q.ipw);
+        P.rs = row_bcast<0>(Q.rs);
+        P.re = row_bcast<0>(Q.re);
+        P.fs = row_bcast<0>(Q.fs);
+        P.corr = ((uint64_t)row_bcast<0>((uint32_t)(Q.corr >> 32)) << 32) | row_bcast<0>((uint32_t)Q.corr);
+    }
+    if (!S.valid || S.bad) P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
+    uint32_t st = P.st;
+    uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
+    uint32_t l4w = NFCS_PATCH_NONE;
+    if (P.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation on lane 0
+        SeqOut o = {0, 0, 0, 0, 0};
+        if (rl == 0) o = seq_update(frame, len);
+        st = row_bcast<0>(o.st) | NFCS_ST_FLAG_OVERLAP;
+        ipw = row_bcast<0>((o.ip_off & 0xFFFFu) | (o.ip_val << 16));
+        l4w = row_bcast<0>((o.l4_off & 0xFFFFu) | (o.l4_val << 16));
+    }
+    // region sums (rows without an L4 region add nothing). rlv is opaque so the per-slot
+    // offsets are recomputed rather than hoisted into ~35 long-lived VGPRs.
+    const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
+    const uint32_t tailfix = P.flags & F_TAIL;
+    uint32_t rlv = rl;
+    asm volatile("" : "+v"(rlv));
+    uint64_t acc = 0;
 #pragma unroll
-                for (int k = 0; k < K0; ++k) {
-                    const uint32_t c = lane + 64u * k;
-                    if (c >= c_lo && c < c_hi) acc += add_chunk(S.b.v[k]);
+    for (int k = 0; k < K; ++k) acc_slot(acc, S.v[k], rlv + 16u * k, lo4, re, tailfix);
+    // continuation batches for frames longer than 16*K chunks (jumbo)
+    const uint32_t nre = (re + 15u) >> 4;
+    const uint32_t cmax = wave_max_rows(nre);
+    for (uint32_t cb = 16u * K; cb < cmax; cb += 16u * K) {
+        uint4 w[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = cb + rlv + 16u * k;
+            w[k] = ld16<NT>((c < nre) ? src + c : &g_zero16);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + 16u * k, lo4, re, tailfix);
+    }
+    const uint64_t z = row_sum64(acc) + P.corr;
+    if (P.flags & F_L4) {
+        uint32_t c = (~fold64(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
+        if ((P.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
+        l4w = P.fs | (c << 16);
+    }
+    // Write back the (at most 4) checksum bytes.
+    //  SM 0: byte stores from lanes 0..3.
+    //  SM 1: each lane whose header chunk holds a field byte rewrites its whole 16-byte chunk
+    //        from registers with the new bytes merged (frames start on 16-byte boundaries, so a
+    //        chunk never holds another frame's bytes): full-sector writes, no partial lines.
+    //  SM 2: as 1, but when the frame starts on a 64-byte boundary the whole 64-byte block(s)
+    //        holding the fields are rewritten (lanes 4b..4b+3 for block b).
+    if (!(DBG & 1) && !(P.flags & F_SEQ)) {
+        if (SM == 0) {
+            if (rl < 4) {
+                const uint32_t w = (rl & 2u) ? l4w : ipw;
+                const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+                if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+            }
+        } else if (rl < 8) {
+            uint4 c = S.v[0];
+            uint32_t touched = 0;
+            const uint32_t offs[2] = {ipw & 0xFFFFu, l4w & 0xFFFFu};
+            const uint32_t vals[2] = {ipw >> 16, l4w >> 16};
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                if (offs[f] == NFCS_PATCH_NONE) continue;
+#pragma unroll
+                for (uint32_t bb = 0; bb < 2; ++bb) {
+                    const uint32_t pos = offs[f] + bb;
+                    const uint32_t val = (vals[f] >> (8 * bb)) & 0xFFu;
+                    const bool mine = (pos >> 4) == rl;
+                    const uint32_t j = (pos >> 2) & 3u, sh = 8u * (pos & 3u);
+                    const uint32_t keep = mine ? ~(0xFFu << sh) : 0xFFFFFFFFu;
+                    const uint32_t put = mine ? (val << sh) : 0u;
+                    if (j == 0) c.x = (c.x & keep) | put;
+                    if (j == 1) c.y = (c.y & keep) | put;
+                    if (j == 2) c.z = (c.z & keep) | put;
+                    if (j == 3) c.w = (c.w & keep) | put;
+                    touched |= (uint32_t)mine << (pos >> 6);
                 }
-                if (has_tail && c_hi < 64u * K0)
-                    for (uint32_t q = hi16 >> 2; 4u * q < re; ++q)
-                        sc += masked_dw(batch_dw<K0>(S.b, q, 0), q, re, P.tailfix);
-                // continuation batches (frames longer than 64*K0 chunks)
-                const uint4* src = (const uint4*)frame;
-                for (uint32_t cb = 64u * K0; cb < nre; cb += 64u * K1) {
-                    Batch<K1> B;
-#pragma unroll
-                    for (int k = 0; k < K1; ++k) {
-                        const uint32_t c = cb + lane + 64u * k;
-                        B.v[k] = *((c < nre) ? src + c : &g_zero16);
-                    }
-#pragma unroll
-                    for (int k = 0; k < K1; ++k) {
-                        const uint32_t c = cb + lane + 64u * k;
-                        if (c >= c_lo && c < c_hi) acc += add_chunk(B.v[k]);
-                    }
-                    if (has_tail && c_hi >= cb && c_hi < cb + 64u * K1)
-                        for (uint32_t q = hi16 >> 2; 4u * q < re; ++q)
-                            sc += masked_dw(batch_dw<K1>(B, q, cb), q, re, P.tailfix);
-                }
-                const uint64_t z = wave_sum64(acc) + sc + P.add - P.sub;
-                uint32_t c = (~fold64(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
-                if (P.udp && c == 0) c = 0xFFFFu;     // 867-871
-                l4_off = P.fs;
-                l4_val = c;
             }
-            if (P.has_ip) {
-                ip_off = P.ip_off;
-                ip_val = P.ip_val;
-            }
-            // stores: lanes 0,1 -> IPv4 field bytes, lanes 2,3 -> L4 field bytes
-            if (lane < 4) {
-                const uint32_t isl4 = lane >> 1;
-                const uint32_t ok = isl4 ? P.has_l4 : P.has_ip;
-                const uint32_t pos = (isl4 ? l4_off : ip_off) + (lane & 1u);
-                const uint32_t val = isl4 ? l4_val : ip_val;
-                if (ok) frame[pos] = (uint8_t)(val >> (8 * (lane & 1u)));
-            }
+            // per-block "touched" bits gathered from the row: bit b set if any lane of block b
+            const uint32_t tb = touched | row_bcast<0>(touched) | row_bcast<1>(touched) |
+                                row_bcast<2>(touched) | row_bcast<3>(touched) | row_bcast<4>(touched) |
+                                row_bcast<5>(touched);
+            const uint32_t ext = (len + 15u) & ~15u;  // frame extent in whole chunks
+            const bool a64 = SM == 2 && (((uintptr_t)frame & 63u) == 0);
+            const uint32_t blk = rl >> 2;
+            const bool block_store = a64 && ((tb >> blk) & 1u) && 64u * (blk + 1) <= ext;
+            if (block_store || touched != 0)
+                ((uint4*)frame)[rl] = c;
         }
     }
-    if (lane == 0) {
-        if (status) status[p] = (uint8_t)st;
+    if (S.valid && rl == 0) {
+        if (status) status[S.p] = (uint8_t)st;
         if (patch) {
             uint2 r;
-            r.x = (ip_off & 0xFFFFu) | (l4_off << 16);
-            r.y = (ip_val & 0xFFFFu) | (l4_val << 16);
-            ((uint2*)patch)[p] = r;
+            r.x = (ipw & 0xFFFFu) | (l4w << 16);
+            r.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
+            ((uint2*)patch)[S.p] = r;
         }
     }
 }
 
-template <int K0, int K1>
-__global__ __launch_bounds__(kBlock) void update_kernel(uint8_t* __restrict__ arena,
-                                                        uint64_t arena_bytes,
-                                                        const nfcs_desc* __restrict__ desc,
-                                                        uint32_t n, uint32_t base16,
-                                                        uint8_t* __restrict__ status,
-                                                        nfcs_patch* __restrict__ patch) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    uint32_t p = blockIdx.x * kWavesPerBlock + rfl(threadIdx.x >> 6);
-    if (p >= n) return;
-    Staged<K0> A;
-    stage<K0>(A, arena, arena_bytes, desc, p, base16, lane);
-    for (;;) {
-        const uint32_t pn = p + nw;
-        const bool more = pn < n && pn > p;
-        // always issue the next batch (re-read p at the end) so the wait count is static
-        Staged<K0> B;
-        stage<K0>(B, arena, arena_bytes, desc, more ? pn : p, base16, lane);
-        process<K0, K1>(A, arena, p, lane, status, patch);
-        if (!more) break;
-        A = B;
-        p = pn;
+// Grid-stride over packets, 16 rows (packets) per 256-thread block. PIPE: the next packet's
+// first batch is issued before the current one is processed (two stages of K slots live).
+template <int K, int NT, bool PIPE, int DBG = 0, int SM = 0>
+__global__ __launch_bounds__(kBlock) void update_rows_kernel(uint8_t* __restrict__ arena,
+                                                             uint64_t arena_bytes,
+                                                             const nfcs_desc* __restrict__ desc,
+                                                             uint32_t n, uint32_t base16,
+                                                             uint8_t* __restrict__ status,
+                                                             nfcs_patch* __restrict__ patch) {
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
+    const uint32_t rowbase4 = (lane & ~15u) * 4u;
+    const uint32_t stride = gridDim.x * (kBlock / 16);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / 16) + rfl(threadIdx.x >> 6) * 4u;
+    if (w0 >= n) return;
+    if (!PIPE) {
+        Desc4 Dn = load_desc4(desc, w0, n);
+        for (uint64_t pw = w0; pw < n; pw += stride) {
+            const Desc4 D = Dn;
+            if (pw + stride < n) Dn = load_desc4(desc, pw + stride, n);  // prefetch (lgkmcnt)
+            RowStage<K> S;
+            row_stage<K, NT>(S, arena, arena_bytes, pick_desc(D, row), pw + row, n, base16, rl);
+            row_process<K, NT, DBG, SM>(S, rl, rowbase4, status, patch);
+        }
+    } else {
+        RowStage<K> A;
+        row_stage<K, NT>(A, arena, arena_bytes, pick_desc(load_desc4(desc, w0, n), row), w0 + row,
+                         n, base16, rl);
+        Desc4 Dn = load_desc4(desc, w0 + stride < n ? w0 + stride : w0, n);
+        for (uint64_t pw = w0; pw < n; pw += stride) {
+            const uint64_t pn = pw + stride;
+            const bool more = pn < n;
+            const Desc4 D = Dn;
+            if (pn + stride < n) Dn = load_desc4(desc, pn + stride, n);
+            RowStage<K> B;  // always staged (a re-read of p at the end) so waits stay counted
+            row_stage<K, NT>(B, arena, arena_bytes, pick_desc(D, row), (more ? pn : pw) + row, n,
+                             base16, rl);
+            row_process<K, NT, DBG, SM>(A, rl, rowbase4, status, patch);
+            A = B;
+        }
+    }
+}
+
+// Split mode, second pass: write the patch records of the checksum pass into the frames. A
+// write-only pass over 8 bytes per packet, so the frame stream of the first pass carries no
+// scattered stores (each write transaction in a read stream costs far more than its bytes).
+__global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restrict__ arena,
+                                                               const nfcs_desc* __restrict__ desc,
+                                                               uint32_t n, uint32_t base16,
+                                                               const nfcs_patch* __restrict__ patch) {
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint2 r = ((const uint2*)patch)[i];
+        const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
+        if (ipo == NFCS_PATCH_NONE && l4o == NFCS_PATCH_NONE) continue;
+        uint8_t* f = arena + ((uint64_t)desc[i].off16 - base16) * 16u;
+        if (ipo != NFCS_PATCH_NONE) {  // l2 + 10: always even
+            *(uint16_t*)(f + ipo) = (uint16_t)(r.y & 0xFFFFu);
+        }
+        if (l4o != NFCS_PATCH_NONE) {  // TCP's field at l4 + 15 is odd
+            if (l4o & 1u) {
+                f[l4o] = (uint8_t)(r.y >> 16);
+                f[l4o + 1] = (uint8_t)(r.y >> 24);
+            } else {
+                *(uint16_t*)(f + l4o) = (uint16_t)(r.y >> 16);
+            }
+        }
     }
 }
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, hipStream_t stream, int variant, int grid) {
+                         nfcs_patch* patch, hipStream_t stream, int variant, int grid,
+                         nfcs_patch* ws) {
     if (n == 0) return hipSuccess;
-    if (grid <= 0) grid = di.cus * 8;  // 8 blocks (32 waves) per CU, grid-stride beyond
-    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    if ((uint32_t)grid > need) grid = (int)need;
+    // One 16-packet block per 256-thread workgroup, as many workgroups as blocks (a grid
+    // that grid-strides over resident workgroups measured 10-15% slower: profiles/).
+    const uint32_t blocks_need = (n + 15u) / 16u;
+    const int g = grid > 0 ? (grid < (int)blocks_need ? grid : (int)blocks_need) : (int)blocks_need;
+#define NFCS_ROWSP(K, NT, PIPE, DBG, SM, PP)                                                     \
+    hipLaunchKernelGGL((update_rows_kernel<K, NT, PIPE, DBG, SM>), dim3(g), dim3(kBlock), 0,     \
+                       stream, arena, arena_bytes, desc, n, base16, status, PP)
+#define NFCS_ROWS(K, NT, PIPE) NFCS_ROWSP(K, NT, PIPE, 0, 0, patch)
     switch (variant) {
     default:
-    case 0:
-        hipLaunchKernelGGL((update_kernel<2, 4>), dim3(grid), dim3(kBlock), 0, stream, arena,
-                           arena_bytes, desc, n, base16, status, patch);
-        break;
-    case 1:
-        hipLaunchKernelGGL((update_kernel<1, 4>), dim3(grid), dim3(kBlock), 0, stream, arena,
-                           arena_bytes, desc, n, base16, status, patch);
-        break;
-    case 2:
-        hipLaunchKernelGGL((update_kernel<2, 8>), dim3(grid), dim3(kBlock), 0, stream, arena,
-                           arena_bytes, desc, n, base16, status, patch);
+    case 0: NFCS_ROWS(6, 2, false); break;  // header slot cached, payload slots evict-first
+    case 1: NFCS_ROWS(6, 0, false); break;  // all loads default policy
+    case 2: NFCS_ROWS(4, 2, false); break;
+    case 3: NFCS_ROWS(6, 2, true); break;   // next packet's batch issued before processing
+    case 4: NFCS_ROWS(6, 1, false); break;  // all loads evict-first
+    case 8: {  // split: checksum pass without frame stores, then the patch pass
+        nfcs_patch* pp = patch ? patch : ws;
+        if (!pp) return hipErrorInvalidValue;
+        NFCS_ROWSP(6, 2, false, 1, 0, pp);
+        int ga = (int)((n + kBlock - 1) / kBlock);
+        if (ga > di.cus * 8) ga = di.cus * 8;
+        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+                           base16, pp);
         break;
     }
+#ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+    case 101: NFCS_ROWSP(6, 2, false, 1, 0, patch); break;  // no frame stores
+    case 102: NFCS_ROWSP(6, 2, false, 2, 0, patch); break;  // no parse (fixed C1 plan)
+    case 103: NFCS_ROWSP(6, 2, false, 3, 0, patch); break;  // neither
+    case 121: NFCS_ROWSP(6, 2, false, 0, 1, patch); break;  // 16-byte chunk write-back
+    case 122: NFCS_ROWSP(6, 2, false, 0, 2, patch); break;  // 64-byte block write-back
+#endif
+    }
+#undef NFCS_ROWS
+#undef NFCS_ROWSP
     return hipGetLastError();
 }
 
@@ -620,6 +883,29 @@ hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint6
     hipLaunchKernelGGL(gen_config_kernel, dim3(grid), dim3(kBlock), 0, stream, config, seed,
                        first, n, arena, arena_bytes, desc);
     return hipGetLastError();
+}
+
+DEV uint64_t wave_sum64(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#define NFCS_DPP_STEP(ctrl)                                                              \
+    {                                                                                    \
+        uint32_t l2_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xF, 0xF, true); \
+        uint32_t h2_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xF, 0xF, true); \
+        uint64_t s_ = ((uint64_t)hi << 32 | lo) + ((uint64_t)h2_ << 32 | l2_);           \
+        lo = (uint32_t)s_;                                                               \
+        hi = (uint32_t)(s_ >> 32);                                                       \
+    }
+    NFCS_DPP_STEP(0xB1)   // quad_perm [1,0,3,2]
+    NFCS_DPP_STEP(0x4E)   // quad_perm [2,3,0,1]
+    NFCS_DPP_STEP(0x141)  // row_half_mirror
+    NFCS_DPP_STEP(0x140)  // row_mirror: every lane of a 16-lane row now holds the row sum
+#undef NFCS_DPP_STEP
+    uint64_t s = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        s += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
+    return s;
 }
 
 // ---- order-independent frame digest (same as oracle nfo_digest) --------------

@@ -63,7 +63,7 @@ def lib() -> ctypes.CDLL:
         L.nfo_config_len.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         L.nfo_config_len.restype = ctypes.c_uint32
         L.nfo_layout_config.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
-                                        ctypes.c_uint32, ctypes.c_void_p]
+                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         L.nfo_layout_config.restype = ctypes.c_uint64
         L.nfo_gen_config.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_uint32, _u8p, ctypes.c_void_p]
@@ -130,14 +130,14 @@ def update_batch(arena: np.ndarray, desc: np.ndarray, nthreads: int = 1,
     return status, result
 
 
-def layout_config(config: int, seed: int, first: int, n: int):
+def layout_config(config: int, seed: int, first: int, n: int, align: int = 16):
     desc = np.zeros(n, dtype=DESC_DTYPE)
-    nbytes = lib().nfo_layout_config(config, seed, first, n, desc.ctypes.data)
+    nbytes = lib().nfo_layout_config(config, seed, first, n, align, desc.ctypes.data)
     return desc, int(nbytes)
 
 
-def gen_config(config: int, seed: int, first: int, n: int):
-    desc, nbytes = layout_config(config, seed, first, n)
+def gen_config(config: int, seed: int, first: int, n: int, align: int = 16):
+    desc, nbytes = layout_config(config, seed, first, n, align)
     arena = np.zeros(max(nbytes, 16), dtype=np.uint8)
     lib().nfo_gen_config(config, seed, first, n, _ptr(arena), desc.ctypes.data)
     return arena, desc

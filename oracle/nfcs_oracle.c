@@ -265,7 +265,9 @@ void nfo_config_frame(int config, uint64_t seed, uint64_t index, uint8_t* f) {
     }
 }
 
-uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n, nfo_desc* desc) {
+uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
+                           nfo_desc* desc) {
+    if (align < 16) align = 16;
     uint64_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t len = nfo_config_len(config, seed, first + i);
@@ -273,7 +275,7 @@ uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n
             desc[i].off16 = (uint32_t)(off >> 4);
             desc[i].len = len;
         }
-        off += ((uint64_t)len + 15) & ~15ULL;
+        off += ((uint64_t)len + align - 1) / align * align;
     }
     return off;
 }

@@ -41,7 +41,8 @@ int nfo_update_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
 /* synthetic configs (spec in DESIGN.md §6) */
 uint32_t nfo_config_len(int config, uint64_t seed, uint64_t index);
 void nfo_config_frame(int config, uint64_t seed, uint64_t index, uint8_t* out /* >= len */);
-uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n, nfo_desc* desc);
+uint64_t nfo_layout_config(int config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
+                           nfo_desc* desc);
 void nfo_gen_config(int config, uint64_t seed, uint64_t first, uint32_t n, uint8_t* arena,
                     const nfo_desc* desc);
 

@@ -1,0 +1,94 @@
+// stream_read.hip — measurement tool (not product): a pure HBM read stream on the same
+// device, giving the achievable read bandwidth that the checksum kernel is compared with.
+//   hipcc --offload-arch=gfx950 -O3 tools/stream_read.hip -o tools/stream_read && tools/stream_read
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_sum(const uint4* __restrict__ p, size_t n16, unsigned long long* out) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * 256;
+    uint64_t acc = 0;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        u32x4 v[U];
+        const u32x4* q = (const u32x4*)p;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(q + i + u * stride) : q[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    for (; i < n16; i += stride) { uint4 v = p[i]; acc += (uint64_t)v.x + v.y + v.z + v.w; }
+    if (acc == 0x123456789ull) *out = acc;  // keep live
+}
+
+// read everything + write 4 bytes per 1504-byte "frame" in place (the checksum kernel's
+// store pattern), or 8 bytes per frame into a separate dense array
+template <int MODE>
+__global__ __launch_bounds__(256) void read_write(uint4* __restrict__ p, size_t n16, uint2* __restrict__ side,
+                                                  unsigned long long* out) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * 256;
+    uint64_t acc = 0;
+    for (; i < n16; i += stride) {
+        uint4 v = p[i];
+        acc += (uint64_t)v.x + v.y + v.z + v.w;
+        const size_t byte = i * 16, f = byte / 1504, fo = byte - f * 1504;
+        if (fo <= 24 && 24 < fo + 16) {  // the chunk holding frame byte 24
+            if (MODE == 1) ((uint8_t*)p)[f * 1504 + 24] = (uint8_t)acc;
+            if (MODE == 2) side[f] = make_uint2((uint32_t)acc, 1u);
+        }
+        if (fo <= 40 && 40 < fo + 16) {
+            if (MODE == 1) ((uint8_t*)p)[f * 1504 + 40] = (uint8_t)acc;
+        }
+    }
+    if (acc == 0x123456789ull) *out = acc;
+}
+
+template <int MODE>
+float run_rw(uint4* p, size_t n16, uint2* side, int grid, unsigned long long* o) {
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w) read_write<MODE><<<grid, 256>>>(p, n16, side, o);
+    float best = 1e9;
+    for (int r = 0; r < 10; ++r) {
+        hipEventRecord(a); read_write<MODE><<<grid, 256>>>(p, n16, side, o); hipEventRecord(b);
+        hipEventSynchronize(b); float ms; hipEventElapsedTime(&ms, a, b); if (ms < best) best = ms;
+    }
+    return best;
+}
+
+template <int U, bool NT>
+float run(const uint4* p, size_t n16, int grid, unsigned long long* o) {
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w) read_sum<U, NT><<<grid, 256>>>(p, n16, o);
+    float best = 1e9;
+    for (int r = 0; r < 10; ++r) {
+        hipEventRecord(a); read_sum<U, NT><<<grid, 256>>>(p, n16, o); hipEventRecord(b);
+        hipEventSynchronize(b); float ms; hipEventElapsedTime(&ms, a, b); if (ms < best) best = ms;
+    }
+    return best;
+}
+
+int main() {
+    const size_t bytes = 1504ull * 1048576ull;  // the C1 arena size
+    uint4* p; unsigned long long* o;
+    hipMalloc(&p, bytes); hipMalloc(&o, 8); hipMemset(p, 1, bytes);
+    hipDeviceProp_t prop; hipGetDeviceProperties(&prop, 0);
+    int cus = prop.multiProcessorCount;
+    const size_t n16 = bytes / 16;
+    int grids[] = {cus * 2, cus * 4, cus * 8, cus * 16, cus * 32};
+    for (int g : grids) {
+        float t1 = run<1, false>(p, n16, g, o), t4 = run<4, false>(p, n16, g, o), t4n = run<4, true>(p, n16, g, o);
+        printf("{\"grid\": %d, \"u1_GBs\": %.1f, \"u4_GBs\": %.1f, \"u4_nt_GBs\": %.1f}\n", g,
+               bytes / t1 / 1e6, bytes / t4 / 1e6, bytes / t4n / 1e6);
+    }
+    uint2* side; hipMalloc(&side, 1048576 * 8);
+    for (int g : grids) {
+        float r0 = run_rw<0>(p, n16, side, g, o), r1 = run_rw<1>(p, n16, side, g, o), r2 = run_rw<2>(p, n16, side, g, o);
+        printf("{\"grid\": %d, \"read_GBs\": %.1f, \"read+inplace4B_GBs\": %.1f, \"read+side8B_GBs\": %.1f}\n", g,
+               bytes / r0 / 1e6, bytes / r1 / 1e6, bytes / r2 / 1e6);
+    }
+    return 0;
+}
