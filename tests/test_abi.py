@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_library_contains_gfx950_code_object():
     blob = open(nf.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
-    assert b"update_kernel" in blob
+    assert b"update_rows_kernel" in blob
 
 
 def test_error_conventions_without_gpu(lib):
