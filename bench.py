@@ -127,7 +127,8 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0):
     except Exception as e:  # pragma: no cover
         return {"value": None, "error": repr(e)}
     kind = "reference" if oracle.ref_available() else "port"
-    n = {0: 1024, 1: 1 << 17, 2: 1 << 14, 3: 1 << 17}[config]
+    # at least ~1.2 GB so the sample streams from DRAM like the GPU batch, not from a large L3
+    n = {0: 1024, 1: 1 << 20, 2: 1 << 17, 3: 1 << 21}[config]
     arena, desc = oracle.gen_config(config, SEED, 0, n)
     nbytes = float(desc["len"].astype(np.float64).sum())
     if kind == "reference":
@@ -151,14 +152,17 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0):
                       f"{threads} threads, g++ -O2, {el:.1f} s"}
 
 
-def load_traffic(config: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+def load_traffic(config: int, n: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
+    for the default batch size of the config; None otherwise."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        t = json.load(open(p))
-        return t.get(f"C{config}")
+        t = json.load(open(p)).get(f"C{config}")
     except (OSError, ValueError):
         return None
+    if not t or n != DEFAULT_PACKETS[config]:
+        return None
+    return t
 
 
 def main():
@@ -213,7 +217,7 @@ def main():
     parity_ok = None if want is None else (got == want)
     parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    traffic = load_traffic(args.config)
+    traffic = load_traffic(args.config, n)
     out = {
         "metric": "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X",
         "value": round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
@@ -231,7 +235,10 @@ def main():
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_ms": round(ev_ms, 4),
+                     "traffic": None if traffic is None else int(traffic["hbm_bytes"]),
+                     "traffic_read_write": None if traffic is None else
+                     [int(traffic["fetch_bytes"]), int(traffic["write_bytes"])],
+                     "kernel_ms": round(ev_ms, 4),
                      "algorithmic_bytes_per_launch": int(algo_bytes)},
         "parity": {"digest": got, "reference_digest": want, "match": parity_ok, "all_ranks": parity_all},
     }
