@@ -1,0 +1,259 @@
+// netflow_amd/packet.hpp — C++ host API for NetFlow++ callers of the checksum path.
+//
+// Mirrors the reference types a caller of Packet::update_checksums() holds:
+//   netflow::PacketBuffer   include/netflow++/packet_buffer.hpp:10-111
+//   netflow::Packet         include/netflow++/packet.hpp:344-918 (ctor/dtor 346-357,
+//                           get_buffer 379, update_checksums 722-890)
+// with the same member names, argument meaning and error behaviour, and adds the batched
+// entry point that the reference lacks:
+//   netflow_amd::update_checksums_batch(Packet* const*, size_t)
+// which gathers the frames into a pinned, 16-byte-aligned arena, runs the gfx950 engine
+// through the C ABI (include/nfcs.h), copies back 8-byte patch records and writes the 2+2
+// checksum bytes into each PacketBuffer in place — bit-exact with the reference.
+//
+// All checksum arithmetic happens on the GPU; there is no CPU fallback. Constructing the
+// engine without a gfx950 device throws std::runtime_error ("fail loudly").
+// Header-only; link with -lnfcs (netflow_amd/libnfcs.so).
+#pragma once
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "nfcs.h"
+
+namespace netflow_amd {
+
+// Same layout and semantics as netflow::PacketBuffer (packet_buffer.hpp:10-111).
+struct PacketBuffer {
+    unsigned char* raw_data_ptr_;
+    size_t capacity_;
+    size_t data_offset_;
+    size_t data_len_;
+    std::atomic<int> ref_count;
+
+    PacketBuffer(size_t capacity, size_t initial_headroom = 0, size_t initial_data_len = 0)
+        : raw_data_ptr_(new unsigned char[capacity]),
+          capacity_(capacity),
+          data_offset_(initial_headroom),
+          data_len_(initial_data_len),
+          ref_count(1) {
+        if (initial_headroom + initial_data_len > capacity) {
+            delete[] raw_data_ptr_;
+            throw std::invalid_argument("Initial headroom + data length exceeds capacity");
+        }
+    }
+    ~PacketBuffer() { delete[] raw_data_ptr_; }
+    PacketBuffer(const PacketBuffer&) = delete;
+    PacketBuffer& operator=(const PacketBuffer&) = delete;
+
+    void increment_ref() { ref_count.fetch_add(1, std::memory_order_relaxed); }
+    bool decrement_ref() { return ref_count.fetch_sub(1, std::memory_order_acq_rel) == 1; }
+
+    unsigned char* get_data_start_ptr() const { return raw_data_ptr_ + data_offset_; }
+    size_t get_data_length() const { return data_len_; }
+    size_t get_capacity() const { return capacity_; }
+    size_t get_headroom() const { return data_offset_; }
+    size_t get_tailroom() const { return capacity_ - (data_offset_ + data_len_); }
+
+    bool set_data_len(size_t new_len) {
+        if (data_offset_ + new_len <= capacity_) {
+            data_len_ = new_len;
+            return true;
+        }
+        return false;
+    }
+    bool prepend_data(size_t n) {
+        if (get_headroom() >= n) { data_offset_ -= n; data_len_ += n; return true; }
+        return false;
+    }
+    bool append_data(size_t n) {
+        if (get_tailroom() >= n) { data_len_ += n; return true; }
+        return false;
+    }
+    bool consume_data_front(size_t n) {
+        if (data_len_ >= n) { data_offset_ += n; data_len_ -= n; return true; }
+        return false;
+    }
+    bool consume_data_end(size_t n) {
+        if (data_len_ >= n) { data_len_ -= n; return true; }
+        return false;
+    }
+    void reset_offsets_and_len(size_t new_offset, size_t new_len) {
+        if (new_offset + new_len <= capacity_) {
+            data_offset_ = new_offset;
+            data_len_ = new_len;
+        } else {
+            throw std::out_of_range("New offset and length exceed buffer capacity in reset_offsets_and_len");
+        }
+    }
+};
+
+class Packet;
+
+// One engine per device: owns the nfcs context plus reusable pinned/device staging. Calls
+// on one engine are serialised by an internal mutex.
+class ChecksumEngine {
+public:
+    explicit ChecksumEngine(int device = 0) {
+        nfcs_ctx* c = nullptr;
+        const int rc = nfcs_ctx_create(device, &c);
+        if (rc != NFCS_OK)
+            throw std::runtime_error(std::string("netflow_amd: no gfx950 engine on device ") +
+                                     std::to_string(device) + ": " + nfcs_strerror(rc));
+        ctx_ = c;
+    }
+    ~ChecksumEngine() {
+        release();
+        nfcs_ctx_destroy(ctx_);
+    }
+    ChecksumEngine(const ChecksumEngine&) = delete;
+    ChecksumEngine& operator=(const ChecksumEngine&) = delete;
+
+    // Process-wide engine on device 0 (created on first use).
+    static ChecksumEngine& instance() {
+        static ChecksumEngine e(0);
+        return e;
+    }
+
+    // Batched Packet::update_checksums(): frames updated in place in their PacketBuffers.
+    // status (optional) receives one NFCS_ST_* byte per packet. Returns 0 or an NFCS_E* code.
+    inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr);
+
+    nfcs_ctx* ctx() const { return ctx_; }
+
+private:
+    void release() {
+        if (h_arena_) nfcs_host_free(ctx_, h_arena_);
+        if (h_desc_) nfcs_host_free(ctx_, h_desc_);
+        if (h_patch_) nfcs_host_free(ctx_, h_patch_);
+        if (d_arena_) nfcs_device_free(ctx_, d_arena_);
+        if (d_desc_) nfcs_device_free(ctx_, d_desc_);
+        if (d_patch_) nfcs_device_free(ctx_, d_patch_);
+        if (d_status_) nfcs_device_free(ctx_, d_status_);
+        h_arena_ = h_desc_ = h_patch_ = d_arena_ = d_desc_ = d_patch_ = d_status_ = nullptr;
+        arena_cap_ = pkt_cap_ = 0;
+    }
+    int reserve(size_t arena_bytes, size_t n) {
+        if (arena_bytes <= arena_cap_ && n <= pkt_cap_) return NFCS_OK;
+        release();
+        arena_cap_ = arena_bytes < (1u << 20) ? (1u << 20) : arena_bytes;
+        pkt_cap_ = n < 4096 ? 4096 : n;
+        int rc = NFCS_OK;
+        if (!rc) rc = nfcs_host_alloc(ctx_, arena_cap_, &h_arena_);
+        if (!rc) rc = nfcs_host_alloc(ctx_, pkt_cap_ * sizeof(nfcs_desc), &h_desc_);
+        if (!rc) rc = nfcs_host_alloc(ctx_, pkt_cap_ * sizeof(nfcs_patch), &h_patch_);
+        if (!rc) rc = nfcs_device_alloc(ctx_, arena_cap_, &d_arena_);
+        if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_ * sizeof(nfcs_desc), &d_desc_);
+        if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_ * sizeof(nfcs_patch), &d_patch_);
+        if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_, &d_status_);
+        if (rc) release();
+        return rc;
+    }
+
+    nfcs_ctx* ctx_ = nullptr;
+    std::mutex mu_;
+    void *h_arena_ = nullptr, *h_desc_ = nullptr, *h_patch_ = nullptr;
+    void *d_arena_ = nullptr, *d_desc_ = nullptr, *d_patch_ = nullptr, *d_status_ = nullptr;
+    size_t arena_cap_ = 0, pkt_cap_ = 0;
+};
+
+// Same interface as netflow::Packet for what the checksum path touches.
+class Packet {
+public:
+    explicit Packet(PacketBuffer* buf) : buffer_(buf) {
+        if (!buffer_) throw std::invalid_argument("PacketBuffer cannot be null.");
+        buffer_->increment_ref();
+    }
+    ~Packet() {
+        if (buffer_) buffer_->decrement_ref();
+    }
+    Packet(const Packet&) = delete;
+    Packet& operator=(const Packet&) = delete;
+    Packet(Packet&& o) noexcept : buffer_(o.buffer_) { o.buffer_ = nullptr; }
+    Packet& operator=(Packet&& o) noexcept {
+        if (this != &o) {
+            if (buffer_) buffer_->decrement_ref();
+            buffer_ = o.buffer_;
+            o.buffer_ = nullptr;
+        }
+        return *this;
+    }
+
+    PacketBuffer* get_buffer() const { return buffer_; }
+
+    // packet.hpp:722. Single packets go through the same GPU engine as a batch of one (a
+    // latency-bound use; batch with update_checksums_batch). void, like the reference.
+    void update_checksums() {
+        if (!buffer_) return;
+        Packet* self = this;
+        const int rc = ChecksumEngine::instance().update_checksums_batch(&self, 1);
+        if (rc != NFCS_OK) throw std::runtime_error(std::string("update_checksums: ") + nfcs_strerror(rc));
+    }
+
+private:
+    PacketBuffer* buffer_;
+};
+
+inline int ChecksumEngine::update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status) {
+    if (n == 0) return NFCS_OK;
+    if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
+    std::lock_guard<std::mutex> lock(mu_);
+    // gather: each frame at a 16-byte aligned offset of one pinned arena
+    size_t bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        bytes += ((b ? b->get_data_length() : 0) + 15) & ~size_t(15);
+    }
+    if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
+    int rc = reserve(bytes + 16, n);
+    if (rc) return rc;
+    uint8_t* arena = static_cast<uint8_t*>(h_arena_);
+    nfcs_desc* desc = static_cast<nfcs_desc*>(h_desc_);
+    size_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        const size_t len = b ? b->get_data_length() : 0;
+        if (len) std::memcpy(arena + off, b->get_data_start_ptr(), len);
+        std::memset(arena + off + len, 0, ((len + 15) & ~size_t(15)) - len);
+        desc[i] = nfcs_desc{static_cast<uint32_t>(off >> 4), static_cast<uint32_t>(len)};
+        off += (len + 15) & ~size_t(15);
+    }
+    const uint32_t m = static_cast<uint32_t>(n);
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_arena_, arena, off ? off : 16))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_desc_, desc, n * sizeof(nfcs_desc)))) return rc;
+    if ((rc = nfcs_update_device(ctx_, static_cast<uint8_t*>(d_arena_), off ? off : 16,
+                                 static_cast<nfcs_desc*>(d_desc_), m,
+                                 static_cast<uint8_t*>(d_status_),
+                                 static_cast<nfcs_patch*>(d_patch_), nullptr)))
+        return rc;
+    if ((rc = nfcs_memcpy_d2h(ctx_, h_patch_, d_patch_, n * sizeof(nfcs_patch)))) return rc;
+    if (status && (rc = nfcs_memcpy_d2h(ctx_, status, d_status_, n))) return rc;
+    // scatter: the 2+2 checksum bytes into each PacketBuffer, IPv4 field first (packet.hpp
+    // writes it first; applying in that order also reproduces IHL < 5 overlaps exactly)
+    const nfcs_patch* pt = static_cast<const nfcs_patch*>(h_patch_);
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        if (!b) continue;
+        unsigned char* f = b->get_data_start_ptr();
+        if (pt[i].ip_off != NFCS_PATCH_NONE) { f[pt[i].ip_off] = pt[i].ip[0]; f[pt[i].ip_off + 1] = pt[i].ip[1]; }
+        if (pt[i].l4_off != NFCS_PATCH_NONE) { f[pt[i].l4_off] = pt[i].l4[0]; f[pt[i].l4_off + 1] = pt[i].l4[1]; }
+    }
+    return NFCS_OK;
+}
+
+// Free-function form on the process-wide engine.
+inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr) {
+    return ChecksumEngine::instance().update_checksums_batch(pkts, n, status);
+}
+inline int update_checksums_batch(const std::vector<Packet*>& pkts, uint8_t* status = nullptr) {
+    return update_checksums_batch(pkts.data(), pkts.size(), status);
+}
+
+}  // namespace netflow_amd

@@ -1,0 +1,76 @@
+// packet_shim_test.cpp — drives include/netflow_amd/packet.hpp the way NetFlow++ code drives
+// netflow::Packet (tests/packet_test.cpp style), reading frames as hex lines on stdin.
+//   cpu     : PacketBuffer / Packet semantics; engine construction must fail loudly w/o GPU
+//   batch   : update_checksums_batch over all frames; prints "<status> <hex>" per frame
+//   single  : Packet::update_checksums() per frame; prints "<hex>" per frame
+#include <netflow_amd/packet.hpp>
+
+#include <cstdio>
+#include <iostream>
+#include <string>
+#include <vector>
+
+static std::vector<uint8_t> unhex(const std::string& s) {
+    std::vector<uint8_t> v;
+    for (size_t i = 0; i + 1 < s.size(); i += 2) v.push_back((uint8_t)std::stoul(s.substr(i, 2), nullptr, 16));
+    return v;
+}
+static std::string hex(const unsigned char* p, size_t n) {
+    static const char* d = "0123456789abcdef";
+    std::string s;
+    for (size_t i = 0; i < n; ++i) { s += d[p[i] >> 4]; s += d[p[i] & 15]; }
+    return s;
+}
+
+static int cpu_checks() {
+    using namespace netflow_amd;
+    int bad = 0;
+    PacketBuffer pb(128, 32, 0);
+    bad += pb.get_headroom() != 32 || pb.get_tailroom() != 96 || pb.ref_count != 1;
+    bad += !pb.set_data_len(96) || pb.set_data_len(97);
+    bad += !pb.prepend_data(4) || pb.get_data_length() != 100 || pb.get_headroom() != 28;
+    bad += !pb.consume_data_front(4) || !pb.consume_data_end(4) || pb.get_data_length() != 92;
+    {
+        Packet p(&pb);
+        bad += pb.ref_count != 2 || p.get_buffer() != &pb;
+        Packet q(std::move(p));
+        bad += pb.ref_count != 2 || q.get_buffer() != &pb || p.get_buffer() != nullptr;
+    }
+    bad += pb.ref_count != 1;
+    try { Packet nullp(nullptr); bad += 1; } catch (const std::invalid_argument&) {}
+    try { PacketBuffer over(8, 4, 8); bad += 1; } catch (const std::invalid_argument&) {}
+    bool threw = false;
+    try { ChecksumEngine e(0); } catch (const std::runtime_error&) { threw = true; }
+    std::printf("engine_without_gpu_throws=%d\n", threw ? 1 : 0);
+    std::printf("api_failures=%d\n", bad);
+    return bad;
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (mode == "cpu") return cpu_checks();
+    std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
+    std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::vector<uint8_t> f = unhex(line);
+        // data window inside a larger buffer with headroom, as the reference's pools allocate
+        bufs.emplace_back(new netflow_amd::PacketBuffer(f.size() + 96, 32, f.size()));
+        if (!f.empty()) std::memcpy(bufs.back()->get_data_start_ptr(), f.data(), f.size());
+        pkts.emplace_back(new netflow_amd::Packet(bufs.back().get()));
+    }
+    std::vector<netflow_amd::Packet*> raw;
+    for (auto& p : pkts) raw.push_back(p.get());
+    std::vector<uint8_t> st(raw.size(), 0xEE);
+    if (mode == "batch") {
+        int rc = netflow_amd::update_checksums_batch(raw, st.data());
+        if (rc) { std::fprintf(stderr, "rc=%d\n", rc); return 2; }
+    } else {
+        for (auto* p : raw) p->update_checksums();
+    }
+    for (size_t i = 0; i < raw.size(); ++i) {
+        auto* b = raw[i]->get_buffer();
+        std::printf("%d %s\n", (int)st[i], hex(b->get_data_start_ptr(), b->get_data_length()).c_str());
+    }
+    return 0;
+}

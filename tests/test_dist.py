@@ -1,0 +1,62 @@
+"""Multi-process path of bench.py on CPU: world_size 2 over gloo (127.0.0.1).
+
+The checksum path shards by packets with no data-path collective: each rank
+owns packets [rank*n, (rank+1)*n) of the same seeded stream, and ranks only meet at the timing
+barriers (max over ranks of the wall time, sum of frame bytes). This checks that harness: the
+shards tile the packet stream exactly, the reductions are right, and per-shard oracle digests
+add up to the digest of the whole stream (the property the N-GPU parity check relies on).
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws),
+                      RANK=str(rank), LOCAL_RANK=str(rank), NFCS_DIST_BACKEND="gloo")
+    import bench
+    import oracle
+    D = bench.Dist(*bench.dist_env())
+    first, n = bench.shard(rank, 4096)
+    D.barrier()
+    mx = D.max(1.5 + rank)
+    total = D.sum(float(n))
+    din, dout, hist = oracle.config_digest(1, bench.SEED, first, n, 1)
+    dsum = D.sum(float(dout % (1 << 40)))  # exact in float64 for 2 ranks
+    D.barrier()
+    D.close()
+    q.put((rank, first, n, mx, total, dout, dsum))
+
+
+@pytest.mark.parametrize("ws", [2])
+def test_two_rank_gloo_harness(ws):
+    import oracle
+    oracle.build(ref=False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # shards tile [0, ws*n) exactly
+    assert [(r[1], r[2]) for r in res] == [(r * 4096, 4096) for r in range(ws)]
+    assert all(r[3] == 1.5 + ws - 1 for r in res)      # max over ranks
+    assert all(r[4] == 4096.0 * ws for r in res)       # sum over ranks
+    # digests are order-independent sums: shard digests add up to the whole stream's digest
+    _, whole, _ = oracle.config_digest(1, 20250620, 0, 4096 * ws, 2)
+    assert (sum(r[5] for r in res) % (1 << 64)) == whole
+    assert all(r[6] == float(sum(x[5] % (1 << 40) for x in res)) for r in res)
