@@ -172,7 +172,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, choices=[0, 1, 2, 3])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config size)")
-    ap.add_argument("--align", type=int, default=16, help="frame start alignment in the arena (16 or 64)")
+    ap.add_argument("--align", type=int, default=128,
+                    help="frame start alignment in the arena: 128 = one L2 line per frame start, as "
+                         "NIC/DPDK buffer rings lay frames out (16 = densely packed)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)

@@ -145,7 +145,8 @@ NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_by
 NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
                                 uint32_t align, nfcs_desc* h_desc, uint64_t* arena_bytes);
 
-/* Fill the frames of a laid-out config batch on the device (d_desc from nfcs_layout_config). */
+/* Fill the frames of a laid-out config batch on the device (d_desc from nfcs_layout_config);
+ * the whole arena is zeroed first, so padding between aligned frames is defined. */
 NFCS_API int nfcs_gen_config_device(nfcs_ctx* ctx, int config, uint64_t seed,
                                     uint64_t first_index, uint32_t n, uint8_t* d_arena,
                                     uint64_t arena_bytes, const nfcs_desc* d_desc, void* stream);

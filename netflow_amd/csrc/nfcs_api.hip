@@ -304,6 +304,8 @@ NFCS_API int nfcs_gen_config_device(nfcs_ctx* c, int config, uint64_t seed, uint
     if (!c || config < 0 || config > 3) return NFCS_EINVAL;
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc) return NFCS_EINVAL;
+    // padding between aligned frame starts is zeroed too, so the arena is fully defined
+    NFCS_HIP(hipMemsetAsync(d_arena, 0, arena_bytes, pick(c, stream)));
     NFCS_HIP(nfcs::launch_gen_config(c->di, config, seed, first, n, d_arena, arena_bytes, d_desc,
                                      pick(c, stream)));
     return NFCS_OK;

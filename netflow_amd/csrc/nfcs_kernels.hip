@@ -39,15 +39,19 @@ namespace nfcs {
 DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// End-around-carry fold of an exact sum to 16 bits (packet.hpp:907-909). Zero stays zero;
-// a nonzero multiple of 0xFFFF folds to 0xFFFF, as in the reference.
+// End-around-carry fold of an exact sum to 16 bits (packet.hpp:907-909), branch-free for sums
+// below 2^48: one 64->33-bit step and three 16-bit steps (extra steps on a value < 0x10000
+// are the identity, so this equals the reference's while loop). Zero stays zero; a nonzero
+// multiple of 0xFFFF folds to 0xFFFF, as in the reference.
 DEV uint32_t fold64(uint64_t s) {
-    s = (s & 0xFFFFFFFFull) + (s >> 32);
-    while (s >> 16) s = (s & 0xFFFFull) + (s >> 16);
-    return (uint32_t)s;
+    uint64_t t = (s & 0xFFFFFFFFull) + (s >> 32);    // <= 0x1_0000_7FFE
+    t = (t & 0xFFFFull) + (t >> 16);                 // <= 0x1FFFF
+    uint32_t u = (uint32_t)t;
+    u = (u & 0xFFFFu) + (u >> 16);                   // <= 0x10000
+    u = (u & 0xFFFFu) + (u >> 16);                   // <= 0xFFFF
+    return u;
 }
 
-// ---- staged chunk registers ------------------------------------------------------------------
 __device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).

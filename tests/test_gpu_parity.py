@@ -82,12 +82,12 @@ def test_fuzz_vs_oracle_fresh_seeds(engine, seed):
     assert np.array_equal(re, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
-def test_config_batch_generator_and_update_vs_oracle(engine, cfg):
+@pytest.mark.parametrize("cfg,align", [(0, 16), (1, 16), (2, 16), (3, 16), (1, 128), (3, 128), (2, 64)])
+def test_config_batch_generator_and_update_vs_oracle(engine, cfg, align):
     n = {0: 1024, 1: 8192, 2: 2048, 3: 16384}[cfg]
-    d_arena, nbytes, d_desc, hdesc = engine.config_batch(cfg, SEED, 12345, n)
+    d_arena, nbytes, d_desc, hdesc = engine.config_batch(cfg, SEED, 12345, n, align)
     gen = d_arena.download(np.uint8, nbytes)
-    o_arena, o_desc = oracle.gen_config(cfg, SEED, 12345, n)
+    o_arena, o_desc = oracle.gen_config(cfg, SEED, 12345, n, align)
     assert np.array_equal(hdesc, o_desc)
     assert np.array_equal(gen, o_arena[:nbytes]), "device generator != oracle generator"
     d_st = engine.alloc(n)
@@ -105,7 +105,7 @@ def test_full_size_digest_matches_reference(engine, cfg):
     g = json.load(open(os.path.join(GOLD, "configs.json")))
     c = g["configs"][str(cfg)]
     n = c["n"]
-    d_arena, nbytes, d_desc, _ = engine.config_batch(cfg, g["seed"], 0, n)
+    d_arena, nbytes, d_desc, _ = engine.config_batch(cfg, g["seed"], 0, n, 128 if cfg in (1, 3) else 16)
     din = engine.digest_device(d_arena, nbytes, d_desc, n, 0)
     assert f"{din:016x}" == c["digest_in"]
     d_st = engine.alloc(n)

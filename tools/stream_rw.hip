@@ -37,6 +37,10 @@ __global__ __launch_bounds__(256) void rw(uint4* __restrict__ p, size_t n16, uns
         if (MODE == 12 && c == 1 && i >= 8 * stride) p[i - 8 * stride] = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
         if (MODE == 13 && c == 1 && i >= 8 * stride) ((uint32_t*)(p + i - 8 * stride))[2] = 0x01010101u;
         if (MODE == 14 && c == 1 && i >= 8 * stride) ((uint8_t*)(p + i - 8 * stride))[8] = 0x01u;
+        if (MODE == 15 && c < 4 && i >= 8 * stride) p[i - 8 * stride] = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+        if (MODE == 16 && c < 8 && i >= 8 * stride) p[i - 8 * stride] = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+        if (MODE == 17 && c < 8 && i >= 64 * stride) p[i - 64 * stride] = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+        if (MODE == 18 && c == 1 && i >= 64 * stride) p[i - 64 * stride] = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
         if (MODE == 9 && c == 1) {
             __hip_atomic_store((unsigned long long*)(p + i), ((unsigned long long)v.y << 32) | v.x,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -75,14 +79,16 @@ int main() {
     (void)hipMemset(p, 1, bytes);
     const size_t n16 = bytes / 16;
     const char* names[] = {"none", "1B", "2x1B", "16B", "64B", "128B", "16B_nt", "64B_nt", "128B_nt", "16B_sc1",
-                           "4B", "2B", "16B_late", "4B_late", "1B_late"};
+                           "4B", "2B", "16B_late", "4B_late", "1B_late", "64B_late", "128B_late",
+                           "128B_later64", "16B_later64"};
     for (int g : {2048, 8192}) {
-        float t[15] = {run<0>(p, n16, g, o), run<1>(p, n16, g, o), run<2>(p, n16, g, o), run<3>(p, n16, g, o),
+        float t[19] = {run<0>(p, n16, g, o), run<1>(p, n16, g, o), run<2>(p, n16, g, o), run<3>(p, n16, g, o),
                        run<4>(p, n16, g, o), run<5>(p, n16, g, o), run<6>(p, n16, g, o), run<7>(p, n16, g, o),
                        run<8>(p, n16, g, o), run<9>(p, n16, g, o), run<10>(p, n16, g, o), run<11>(p, n16, g, o),
-                       run<12>(p, n16, g, o), run<13>(p, n16, g, o), run<14>(p, n16, g, o)};
+                       run<12>(p, n16, g, o), run<13>(p, n16, g, o), run<14>(p, n16, g, o),
+                       run<15>(p, n16, g, o), run<16>(p, n16, g, o), run<17>(p, n16, g, o), run<18>(p, n16, g, o)};
         printf("{\"grid\": %d", g);
-        for (int m = 0; m < 15; ++m) printf(", \"%s\": %.0f", names[m], bytes / t[m] / 1e6);
+        for (int m = 0; m < 19; ++m) printf(", \"%s\": %.0f", names[m], bytes / t[m] / 1e6);
         printf("}\n");
     }
     return 0;
