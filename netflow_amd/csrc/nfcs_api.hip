@@ -36,6 +36,14 @@ struct nfcs_ctx {
     int grid = 0;
     nfcs_patch* ws = nullptr;  // split-mode patch workspace (grown on demand)
     size_t ws_cap = 0;         // records
+    uint32_t* queue = nullptr; // kQueueSlots x kQueueWords work-queue counters
+    uint32_t qslot = 0;
+    nfcs::Work work(size_t) {
+        nfcs::Work w;
+        w.patch = ws;
+        w.queue = queue + (size_t)(qslot++ % (nfcs::kQueueSlots - kSlots)) * nfcs::kQueueWords;
+        return w;
+    }
 };
 
 namespace {
@@ -51,6 +59,14 @@ hipError_t ensure_ws(nfcs_ctx* c, size_t n) {
     hipError_t e = hipMalloc(&c->ws, cap * sizeof(nfcs_patch));
     if (e == hipSuccess) c->ws_cap = cap;
     return e;
+}
+
+// host pipeline slot s: its own patch buffer as split workspace, its own queue slot
+nfcs::Work host_work(nfcs_ctx* c, int s) {
+    nfcs::Work w;
+    w.patch = c->d_patch[s];
+    w.queue = c->queue + (size_t)(nfcs::kQueueSlots - 1 - s) * nfcs::kQueueWords;
+    return w;
 }
 
 int hip_fail(hipError_t e) {
@@ -140,6 +156,9 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     c->grid = env_int("NFCS_GRID", 0);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_digest, sizeof(uint64_t));
+    const size_t qbytes = sizeof(uint32_t) * nfcs::kQueueWords * nfcs::kQueueSlots;
+    if (e == hipSuccess) e = hipMalloc(&c->queue, qbytes);
+    if (e == hipSuccess) e = hipMemset(c->queue, 0, qbytes);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
@@ -168,6 +187,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     }
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->queue) (void)hipFree(c->queue);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -185,7 +205,7 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     NFCS_HIP(ensure_ws(c, n));
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
-                                 pick(c, stream), c->variant, c->grid, c->ws));
+                                 pick(c, stream), c->variant, c->grid, c->work(n)));
     return NFCS_OK;
 }
 
@@ -265,7 +285,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         NFCS_HIP(nfcs::launch_update(c->di, c->d_arena[s], k.bytes, c->d_desc[s], m,
                                      (uint32_t)(base >> 4), c->d_status[s],
                                      patch_only ? c->d_patch[s] : nullptr, st, c->variant,
-                                     c->grid, c->d_patch[s]));
+                                     c->grid, host_work(c, s)));
         if (patch_only) {
             NFCS_HIP(hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
                                     hipMemcpyDeviceToHost, st));
@@ -378,7 +398,7 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,
-                                     st, c->variant, c->grid, c->ws));
+                                     st, c->variant, c->grid, c->work(n)));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

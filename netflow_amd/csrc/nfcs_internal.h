@@ -27,10 +27,18 @@ struct DevInfo {
     char arch[64] = {0};
 };
 
+// Per-context device workspace handed to the checksum launch.
+struct Work {
+    nfcs_patch* patch = nullptr;  // split mode: patch records of the checksum pass
+    uint32_t* queue = nullptr;    // work-queue counters (kQueueWords, zero; kernels re-zero them)
+};
+constexpr int kQueueWords = 9 * 32;  // 8 per-XCD counters + a finish counter, 128 B apart
+constexpr int kQueueSlots = 16;      // rotating, so launches on different streams do not share
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, hipStream_t stream, int variant, int grid,
-                         nfcs_patch* ws);
+                         const Work& work);
 
 // variants that stage patch records in a context workspace (split mode)
 inline bool variant_needs_ws(int variant) { return variant == 8; }

@@ -555,13 +555,14 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 }
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
-// (no parse), 3 = both.
+// (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
 template <int K, int NT, int DBG = 0, int SM = 0>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* patch) {
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
+    if (DBG & 4) __builtin_amdgcn_s_setprio(3);  // finish the compute phase first
     RPlan P;
     if (DBG & 2) {
         P = rplan_none(NFCS_ST_V4_UDP);
@@ -624,8 +625,8 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     //  SM 1: each lane whose header chunk holds a field byte rewrites its whole 16-byte chunk
     //        from registers with the new bytes merged (frames start on 16-byte boundaries, so a
     //        chunk never holds another frame's bytes): full-sector writes, no partial lines.
-    //  SM 2: as 1, but when the frame starts on a 64-byte boundary the whole 64-byte block(s)
-    //        holding the fields are rewritten (lanes 4b..4b+3 for block b).
+    //  SM 3: as 1, the whole first 128-byte line when the frame owns it; SM 4: field dwords
+    //  SM 5/6/7: as 1/4/3 with the chunk re-loaded right before the store.
     if (!(DBG & 1) && !(P.flags & F_SEQ)) {
         if (SM == 0) {
             if (rl < 4) {
@@ -634,40 +635,53 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                 if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
             }
         } else if (rl < 8) {
-            uint4 c = S.v[0];
-            uint32_t touched = 0;
+            // field bytes that fall into this lane's header chunk (data independent)
             const uint32_t offs[2] = {ipw & 0xFFFFu, l4w & 0xFFFFu};
             const uint32_t vals[2] = {ipw >> 16, l4w >> 16};
+            uint32_t keep[4] = {~0u, ~0u, ~0u, ~0u}, put[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
-                if (offs[f] == NFCS_PATCH_NONE) continue;
 #pragma unroll
                 for (uint32_t bb = 0; bb < 2; ++bb) {
                     const uint32_t pos = offs[f] + bb;
-                    const uint32_t val = (vals[f] >> (8 * bb)) & 0xFFu;
-                    const bool mine = (pos >> 4) == rl;
+                    const bool mine = offs[f] != NFCS_PATCH_NONE && (pos >> 4) == rl;
                     const uint32_t j = (pos >> 2) & 3u, sh = 8u * (pos & 3u);
-                    const uint32_t keep = mine ? ~(0xFFu << sh) : 0xFFFFFFFFu;
-                    const uint32_t put = mine ? (val << sh) : 0u;
-                    if (j == 0) c.x = (c.x & keep) | put;
-                    if (j == 1) c.y = (c.y & keep) | put;
-                    if (j == 2) c.z = (c.z & keep) | put;
-                    if (j == 3) c.w = (c.w & keep) | put;
-                    touched |= (uint32_t)mine << (pos >> 6);
+                    const uint32_t val = (vals[f] >> (8 * bb)) & 0xFFu;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        const bool hit = mine && j == q;
+                        keep[q] &= hit ? ~(0xFFu << sh) : ~0u;
+                        put[q] |= hit ? (val << sh) : 0u;
+                    }
                 }
             }
-            // per-block "touched" bits gathered from the row: bit b set if any lane of block b
-            const uint32_t tb = touched | row_bcast<0>(touched) | row_bcast<1>(touched) |
-                                row_bcast<2>(touched) | row_bcast<3>(touched) | row_bcast<4>(touched) |
-                                row_bcast<5>(touched);
-            const uint32_t ext = (len + 15u) & ~15u;  // frame extent in whole chunks
-            const bool a64 = SM == 2 && (((uintptr_t)frame & 63u) == 0);
-            const uint32_t blk = rl >> 2;
-            const bool block_store = a64 && ((tb >> blk) & 1u) && 64u * (blk + 1) <= ext;
-            if (block_store || touched != 0)
+            const uint32_t tm = (keep[0] != ~0u ? 1u : 0u) | (keep[1] != ~0u ? 2u : 0u) |
+                                (keep[2] != ~0u ? 4u : 0u) | (keep[3] != ~0u ? 8u : 0u);
+            // SM 3/7: the whole first L2 line (every field lies in bytes < 128) when the frame
+            // owns it; SM 5/6/7 re-load the chunk just before the store so the store finds its
+            // line in L2 (a store to a line not in L2 stalls the read stream, profiles/)
+            const bool line = (SM == 3 || SM == 7) && (((uintptr_t)frame & 127u) == 0) && len >= 128u;
+            const bool st16 = line || tm != 0;
+            uint4 c = S.v[0];
+            if (SM >= 5 && st16) {
+                c = ld16<0>((const uint4*)frame + rl);
+            }
+            c.x = (c.x & keep[0]) | put[0];
+            c.y = (c.y & keep[1]) | put[1];
+            c.z = (c.z & keep[2]) | put[2];
+            c.w = (c.w & keep[3]) | put[3];
+            if (SM == 4 || SM == 6) {  // only the dwords that hold field bytes
+                uint32_t* q = (uint32_t*)((uint4*)frame + rl);
+                if (tm & 1u) q[0] = c.x;
+                if (tm & 2u) q[1] = c.y;
+                if (tm & 4u) q[2] = c.z;
+                if (tm & 8u) q[3] = c.w;
+            } else if (st16) {
                 ((uint4*)frame)[rl] = c;
+            }
         }
     }
+    if (DBG & 4) __builtin_amdgcn_s_setprio(0);
     if (S.valid && rl == 0) {
         if (status) status[S.p] = (uint8_t)st;
         if (patch) {
@@ -681,8 +695,8 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 
 // Grid-stride over packets, 16 rows (packets) per 256-thread block. PIPE: the next packet's
 // first batch is issued before the current one is processed (two stages of K slots live).
-template <int K, int NT, bool PIPE, int DBG = 0, int SM = 0>
-__global__ __launch_bounds__(kBlock) void update_rows_kernel(uint8_t* __restrict__ arena,
+template <int K, int NT, bool PIPE, int DBG = 0, int SM = 0, int OCC = 1>
+__global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
                                                              uint64_t arena_bytes,
                                                              const nfcs_desc* __restrict__ desc,
                                                              uint32_t n, uint32_t base16,
@@ -699,7 +713,9 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(uint8_t* __restrict
             const Desc4 D = Dn;
             if (pw + stride < n) Dn = load_desc4(desc, pw + stride, n);  // prefetch (lgkmcnt)
             RowStage<K> S;
+            if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
             row_stage<K, NT>(S, arena, arena_bytes, pick_desc(D, row), pw + row, n, base16, rl);
+            if (DBG & 8) __builtin_amdgcn_s_setprio(0);
             row_process<K, NT, DBG, SM>(S, rl, rowbase4, status, patch);
         }
     } else {
@@ -717,6 +733,78 @@ __global__ __launch_bounds__(kBlock) void update_rows_kernel(uint8_t* __restrict
                              base16, rl);
             row_process<K, NT, DBG, SM>(A, rl, rowbase4, status, patch);
             A = B;
+        }
+    }
+}
+
+// Work-queue form: a resident grid of waves, each taking four-packet units from per-XCD
+// atomic counters (workgroups are dispatched round-robin over the 8 XCDs, so blockIdx & 7 is
+// the XCD and every XCD streams its own contiguous eighth of the batch; a drained XCD steals
+// from the next). The next unit's counter value and descriptors are fetched while the current
+// unit's frames are in flight, so a wave goes from one packet's compute straight into the next
+// packet's loads: no wave launch and no descriptor round trip between packets. The last wave
+// to finish re-zeroes the counters for the next launch.
+DEV uint32_t q_take(uint32_t* q, uint32_t x) {  // lane 0 takes a unit; result stays in a VGPR
+    uint32_t v = 0;
+    if ((threadIdx.x & 63u) == 0)
+        v = __hip_atomic_fetch_add(q + 32u * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+
+template <int K, int NT, int DBG = 0, int SM = 0>
+__global__ __launch_bounds__(kBlock) void update_queue_kernel(uint8_t* __restrict__ arena,
+                                                              uint64_t arena_bytes,
+                                                              const nfcs_desc* __restrict__ desc,
+                                                              uint32_t n, uint32_t base16,
+                                                              uint8_t* __restrict__ status,
+                                                              nfcs_patch* __restrict__ patch,
+                                                              uint32_t* __restrict__ q) {
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
+    const uint32_t rowbase4 = (lane & ~15u) * 4u;
+    const uint32_t units = (n + 3u) >> 2;
+    const uint32_t per = (units + 7u) >> 3;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    auto cnt = [&](uint32_t x) -> uint32_t {
+        const uint32_t lo = x * per;
+        return lo >= units ? 0u : min(per, units - lo);
+    };
+    uint32_t x = blockIdx.x & 7u, tries = 0;
+    // blocking take (first unit, and steals once an XCD's range is drained)
+    auto take_next = [&](uint32_t l) -> uint32_t {
+        for (;;) {
+            if (l < cnt(x)) return x * per + l;
+            x = (x + 1u) & 7u;
+            if (++tries >= 8u) return kNone;
+            l = rfl(q_take(q, x));
+        }
+    };
+    uint32_t cur = take_next(rfl(q_take(q, x)));
+    if (cur != kNone) {
+        Desc4 D = load_desc4(desc, (uint64_t)cur * 4u, n);
+        uint32_t pend = q_take(q, x);
+        for (;;) {
+            const uint64_t pw = (uint64_t)cur * 4u;
+            RowStage<K> S;
+            row_stage<K, NT>(S, arena, arena_bytes, pick_desc(D, row), pw + row, n, base16, rl);
+            const uint32_t nxt = take_next(rfl(pend));  // counted wait: the frames stay in flight
+            Desc4 Dn = D;
+            if (nxt != kNone) {
+                Dn = load_desc4(desc, (uint64_t)nxt * 4u, n);
+                pend = q_take(q, x);
+            }
+            row_process<K, NT, DBG, SM>(S, rl, rowbase4, status, patch);
+            if (nxt == kNone) break;
+            cur = nxt;
+            D = Dn;
+        }
+    }
+    if (lane == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(q + 32u * 8u, 1u, __ATOMIC_ACQ_REL,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x * (kBlock / kWave) - 1u) {
+#pragma unroll
+            for (uint32_t i = 0; i <= 8u; ++i)
+                __hip_atomic_store(q + 32u * i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -750,15 +838,22 @@ __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restri
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, hipStream_t stream, int variant, int grid,
-                         nfcs_patch* ws) {
+                         const Work& work) {
+    nfcs_patch* ws = work.patch;
     if (n == 0) return hipSuccess;
     // One 16-packet block per 256-thread workgroup, as many workgroups as blocks (a grid
     // that grid-strides over resident workgroups measured 10-15% slower: profiles/).
     const uint32_t blocks_need = (n + 15u) / 16u;
     const int g = grid > 0 ? (grid < (int)blocks_need ? grid : (int)blocks_need) : (int)blocks_need;
-#define NFCS_ROWSP(K, NT, PIPE, DBG, SM, PP)                                                     \
-    hipLaunchKernelGGL((update_rows_kernel<K, NT, PIPE, DBG, SM>), dim3(g), dim3(kBlock), 0,     \
+#define NFCS_ROWSO(K, NT, PIPE, DBG, SM, OCC, PP)                                                \
+    hipLaunchKernelGGL((update_rows_kernel<K, NT, PIPE, DBG, SM, OCC>), dim3(g), dim3(kBlock), 0, \
                        stream, arena, arena_bytes, desc, n, base16, status, PP)
+#define NFCS_ROWSP(K, NT, PIPE, DBG, SM, PP) NFCS_ROWSO(K, NT, PIPE, DBG, SM, 1, PP)
+    // work-queue form: resident grid (5 waves per SIMD at this kernel's register count)
+    const int gq = grid > 0 ? grid : di.cus * 5;
+#define NFCS_QUEUE(K, NT, DBG, SM)                                                              \
+    hipLaunchKernelGGL((update_queue_kernel<K, NT, DBG, SM>), dim3(gq), dim3(kBlock), 0, stream, \
+                       arena, arena_bytes, desc, n, base16, status, patch, work.queue)
 #define NFCS_ROWS(K, NT, PIPE) NFCS_ROWSP(K, NT, PIPE, 0, 0, patch)
     switch (variant) {
     default:
@@ -782,11 +877,28 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 102: NFCS_ROWSP(6, 2, false, 2, 0, patch); break;  // no parse (fixed C1 plan)
     case 103: NFCS_ROWSP(6, 2, false, 3, 0, patch); break;  // neither
     case 121: NFCS_ROWSP(6, 2, false, 0, 1, patch); break;  // 16-byte chunk write-back
-    case 122: NFCS_ROWSP(6, 2, false, 0, 2, patch); break;  // 64-byte block write-back
+    case 123: NFCS_ROWSP(6, 2, false, 0, 3, patch); break;  // 128-byte header line write-back
+    case 124: NFCS_ROWSP(6, 2, false, 0, 4, patch); break;  // field dwords only
+    case 125: NFCS_ROWSP(6, 1, false, 0, 3, patch); break;  // 123 with all loads nt
+    case 126: NFCS_ROWSP(6, 0, false, 0, 3, patch); break;  // 123 with all loads default
+    case 127: NFCS_ROWSP(6, 2, false, 0, 5, patch); break;  // re-load + 16-byte chunk store
+    case 128: NFCS_ROWSP(6, 2, false, 0, 6, patch); break;  // re-load + field dword stores
+    case 129: NFCS_ROWSP(6, 2, false, 0, 7, patch); break;  // re-load + 128-byte line store
+    case 150: NFCS_QUEUE(6, 2, 0, 0); break;   // work queue
+    case 151: NFCS_QUEUE(6, 2, 1, 0); break;   // work queue, no frame stores
+    case 152: NFCS_QUEUE(6, 2, 4, 0); break;   // work queue, high priority compute phase
+    case 141: NFCS_ROWSP(6, 2, false, 4, 0, patch); break;  // high priority compute phase
+    case 142: NFCS_ROWSP(6, 2, false, 8, 0, patch); break;  // high priority load issue
+    case 143: NFCS_ROWSP(6, 2, false, 4, 4, patch); break;  // 141 + field dword stores
+    case 131: NFCS_ROWSO(6, 2, false, 0, 0, 6, patch); break;  // >= 6 waves per SIMD
+    case 132: NFCS_ROWSO(6, 2, false, 0, 0, 8, patch); break;  // >= 8 waves per SIMD
+    case 133: NFCS_ROWSO(6, 2, false, 0, 3, 8, patch); break;  // 132 + line write-back
 #endif
     }
 #undef NFCS_ROWS
 #undef NFCS_ROWSP
+#undef NFCS_ROWSO
+#undef NFCS_QUEUE
     return hipGetLastError();
 }
 
