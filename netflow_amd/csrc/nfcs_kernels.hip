@@ -39,19 +39,6 @@ namespace nfcs {
 DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// End-around-carry fold of an exact sum to 16 bits (packet.hpp:907-909), branch-free for sums
-// below 2^48: one 64->33-bit step and three 16-bit steps (extra steps on a value < 0x10000
-// are the identity, so this equals the reference's while loop). Zero stays zero; a nonzero
-// multiple of 0xFFFF folds to 0xFFFF, as in the reference.
-DEV uint32_t fold64(uint64_t s) {
-    uint64_t t = (s & 0xFFFFFFFFull) + (s >> 32);    // <= 0x1_0000_7FFE
-    t = (t & 0xFFFFull) + (t >> 16);                 // <= 0x1FFFF
-    uint32_t u = (uint32_t)t;
-    u = (u & 0xFFFFu) + (u >> 16);                   // <= 0x10000
-    u = (u & 0xFFFFu) + (u >> 16);                   // <= 0xFFFF
-    return u;
-}
-
 __device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
@@ -156,23 +143,24 @@ __device__ __noinline__ SeqOut seq_update(uint8_t* f, uint32_t len) {
 }
 
 // ---- region accumulation ---------------------------------------------------------------------
-// The L4 region [rs, re) is summed as LE dwords starting at lo4 = rs & ~3, in three parts:
-//   head: dwords in [lo4, min(lo16, re))   scalar, from the header registers (lo16 <= 80)
-//   body: full chunks in [lo16, hi16)      vector, unmasked uint4 adds into a u64 per lane
-//   tail: dwords in [hi16, re) if hi16 >= lo16: scalar, readlane of the last partial chunk
-// with lo16 = round_up(lo4, 16), hi16 = round_down(re, 16). The odd trailing byte is in the
-// head or the tail (re is odd, so never 16-aligned), where it gets its +255*b.
-DEV uint64_t masked_dw(uint32_t d, uint32_t q, uint32_t re, uint32_t tailfix) {
-    const int n = (int)re - (int)(4u * q);
-    const uint32_t m = n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : ((1u << (8 * n)) - 1u));
-    uint64_t a = d & m;
-    const uint32_t t = re - 1;
-    if (tailfix && (t >> 2) == q) a += 255ull * ((d >> (8 * (t & 3u))) & 0xFFu);
-    return a;
+// The L4 region is summed as 16-bit little-endian words: v_sad_u16(d, 0, acc) adds both
+// halves of a dword to a u32 accumulator in one instruction, with no carry chain. The word
+// sum is congruent to the dword sum mod 0xFFFF (65536 = 1 mod 0xFFFF) and both are zero
+// exactly when every byte is, so they fold to the same checksum; it cannot overflow 32 bits
+// (a region ends before l4 + 65,536 < 65,614 bytes: 16,404 dwords x 131,070 < 2^32).
+DEV uint32_t wsum(uint32_t d, uint32_t acc) { return __builtin_amdgcn_sad_u16(d, 0u, acc); }
+
+DEV uint32_t add_chunk(const uint4& v, uint32_t acc) {
+    return wsum(v.w, wsum(v.z, wsum(v.y, wsum(v.x, acc))));
 }
 
-DEV uint64_t add_chunk(const uint4& v) {
-    return ((uint64_t)v.x + v.y) + ((uint64_t)v.z + v.w);
+// End-around-carry fold of an exact sum to 16 bits (packet.hpp:907-909), branch-free: two
+// steps take any u32 below 0x10000 (a further step on such a value is the identity, so this
+// equals the reference's while loop). Zero stays zero; a nonzero multiple of 0xFFFF folds to
+// 0xFFFF, as in the reference.
+DEV uint32_t fold32(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);  // <= 0x1FFFE
+    return (s & 0xFFFFu) + (s >> 16);
 }
 
 // =============================================================================================
@@ -186,31 +174,38 @@ DEV uint64_t add_chunk(const uint4& v) {
 // ds_bpermute (runtime offsets: IP options, IPv6); the row sum is four DPP steps.
 // =============================================================================================
 
-template <int L>
-DEV uint32_t row_bcast(uint32_t x) {  // lane L of this lane's 16-lane row
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + L, 0xF, 0xF, false);
+// Lane L of this lane's packet row. R = 16: one DPP row_newbcast. R = 8 (two packets per DPP
+// row): row_newbcast L into banks 0-1 (lanes 0-7), row_newbcast 8+L into banks 2-3 (8-15).
+template <int L, int R = 16>
+DEV uint32_t row_bcast(uint32_t x) {
+    static_assert(R == 16 || R == 8, "row width");
+    if (R == 16) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + L, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)x, 0x150 + (L & 7), 0xF, 0x3, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(lo, (int)x, 0x158 + (L & 7), 0xF, 0xC, false);
 }
 
-// Per-lane view of the header bytes [0, 256) of the row's packet: lane rl of the row holds
-// chunk rl (frame bytes 16rl .. 16rl+15) of slot 0.
+// Per-lane view of the header bytes [0, 16R) of the row's packet: lane rl of the row holds
+// chunk rl (frame bytes 16rl .. 16rl+15) of slot 0. Every header field the plan reads lies
+// below byte 128, so R = 8 rows see all of them.
+template <int R>
 struct RowHdr {
     uint4 c0;
     uint32_t rowbase4;  // byte address of lane 0 of this row, for ds_bpermute
     DEV uint32_t dw(uint32_t q) const {
         const uint32_t x = comp(c0, q & 3u);
         if (__builtin_constant_p(q)) {
-            switch ((q >> 2) & 15u) {
-            case 0: return row_bcast<0>(x);   case 1: return row_bcast<1>(x);
-            case 2: return row_bcast<2>(x);   case 3: return row_bcast<3>(x);
-            case 4: return row_bcast<4>(x);   case 5: return row_bcast<5>(x);
-            case 6: return row_bcast<6>(x);   case 7: return row_bcast<7>(x);
-            case 8: return row_bcast<8>(x);   case 9: return row_bcast<9>(x);
-            case 10: return row_bcast<10>(x); case 11: return row_bcast<11>(x);
-            case 12: return row_bcast<12>(x); case 13: return row_bcast<13>(x);
-            case 14: return row_bcast<14>(x); default: return row_bcast<15>(x);
+            switch ((q >> 2) & (R - 1)) {
+            case 0: return row_bcast<0, R>(x);   case 1: return row_bcast<1, R>(x);
+            case 2: return row_bcast<2, R>(x);   case 3: return row_bcast<3, R>(x);
+            case 4: return row_bcast<4, R>(x);   case 5: return row_bcast<5, R>(x);
+            case 6: return row_bcast<6, R>(x);   case 7: return row_bcast<7, R>(x);
+            case 8: return row_bcast<8, R>(x);   case 9: return row_bcast<9, R>(x);
+            case 10: return row_bcast<10, R>(x); case 11: return row_bcast<11, R>(x);
+            case 12: return row_bcast<12, R>(x); case 13: return row_bcast<13, R>(x);
+            case 14: return row_bcast<14, R>(x); default: return row_bcast<15, R>(x);
             }
         }
-        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rowbase4 + ((q >> 2) & 15u) * 4u), (int)x);
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rowbase4 + ((q >> 2) & (R - 1)) * 4u), (int)x);
     }
     DEV uint32_t b(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 3u))) & 0xFFu; }
     DEV uint32_t le16(uint32_t o) const { return (dw(o >> 2) >> (8 * (o & 2u))) & 0xFFFFu; }
@@ -224,7 +219,7 @@ struct RPlan {
     uint32_t flags;  // F_*
     uint32_t ipw;    // ip_off | ip_val << 16
     uint32_t rs, re, fs;
-    uint64_t corr;   // pseudo-header add minus over-counted bytes (two's complement)
+    uint32_t corr;   // pseudo-header words minus over-counted bytes (two's complement)
 };
 
 DEV RPlan rplan_none(uint32_t st) {
@@ -245,11 +240,11 @@ DEV uint4 strip_tag(const uint4& c, bool tagged) {
                       (c.z & ~m) | (c.w & m), (c.w & ~m) | (nx & m));
 }
 
-using View = RowHdr;
 
 // L4 branch of packet.hpp:773-889 in view coordinates with compile-time l2 = 14 and l4
 // (34 for IPv4 with IHL 5, 54 for IPv6); sh = 4 for tagged frames shifts the frame offsets.
-DEV RPlan fast_l4(const View& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l4, uint32_t proto,
+template <int R>
+DEV RPlan fast_l4(const RowHdr<R>& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l4, uint32_t proto,
                   uint32_t sh) {
     const uint32_t l2 = 14, ihl4 = 20;
     const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
@@ -285,7 +280,7 @@ DEV RPlan fast_l4(const View& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l
     } else {
         return P;
     }
-    uint64_t add = 0;
+    uint32_t add = 0;
     if (proto != 1) {  // pseudo-header in the LE domain (797-816 / 840-859)
         add = bswap16(proto) + bswap16(L);
         if (v4) {
@@ -299,9 +294,9 @@ DEV RPlan fast_l4(const View& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l
     // over-counted bytes: the LE word before l4 when l4 = 2 mod 4 (sh keeps the parity), and
     // the raw checksum field bytes the reference zeroes first (795 / 838 / 885)
     const uint32_t re = l4 + L;
-    uint64_t sub = ((l4 + sh) & 2u) ? V.le16(l4 - 2) : 0u;
-    if (fs < re) sub += (uint64_t)V.b(fs) << (((fs + sh) & 1u) ? 8 : 0);
-    if (fs + 1 < re) sub += (uint64_t)V.b(fs + 1) << (((fs + 1 + sh) & 1u) ? 8 : 0);
+    uint32_t sub = ((l4 + sh) & 2u) ? V.le16(l4 - 2) : 0u;
+    if (fs < re) sub += V.b(fs) << (((fs + sh) & 1u) ? 8 : 0);
+    if (fs + 1 < re) sub += V.b(fs + 1) << (((fs + 1 + sh) & 1u) ? 8 : 0);
     const uint32_t t = re - 1;
     if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
     P.st = st;
@@ -315,22 +310,23 @@ DEV RPlan fast_l4(const View& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t l
 
 // Common headers with compile-time offsets: untagged / 802.1Q; IPv4 with IHL 5; IPv6; non-IP.
 // Returns F_SEQ in flags for everything else (IHL != 5: options, IHL < 5, past the frame).
+template <int R>
 DEV RPlan fast_plan(const uint4& c0, uint32_t rowbase4, uint32_t len) {
-    const RowHdr h{c0, rowbase4};
+    const RowHdr<R> h{c0, rowbase4};
     const bool tagged = (len >= 14) && h.be16(12) == 0x8100u;  // ethernet(): l2 = 18
     const uint32_t sh = tagged ? 4u : 0u;
-    const View V{strip_tag(c0, tagged), rowbase4};
+    const RowHdr<R> V{strip_tag(c0, tagged), rowbase4};
     const uint32_t lenv = len - sh;  // len >= 14 whenever tagged
     const uint32_t b0 = V.b(14);
     if (len >= 14 + sh && lenv >= 34 && (b0 >> 4) == 4) {  // 728-734: IPv4 by nibble
         if ((b0 & 15u) != 5) return rplan_none(NFCS_ST_NONE | (F_SEQ << 8));
-        uint64_t s = 0;  // 739-740: header checksum, field zeroed
+        uint32_t s = 0;  // 739-740: header checksum, field zeroed
 #pragma unroll
         for (uint32_t w = 0; w < 20; w += 2)
             if (w != 10) s += V.le16(14 + w);
         RPlan P = rplan_none(NFCS_ST_V4);
         P.flags = F_IP;
-        P.ipw = (24u + sh) | (((~fold64(s)) & 0xFFFFu) << 16);
+        P.ipw = (24u + sh) | (((~fold32(s)) & 0xFFFFu) << 16);
         return fast_l4(V, P, lenv, 1u, 34u, V.b(23), sh);
     }
     // 741-765: effective EtherType (after one tag) must be IPv6 and the nibble 6
@@ -403,16 +399,16 @@ __device__ __noinline__ RPlan slow_plan(const uint8_t* f, uint32_t len) {
     } else {
         return P;
     }
-    uint64_t add = 0;
+    uint32_t add = 0;
     if (proto != 1) {
         add = bswap16(proto) + bswap16(L);
         const uint32_t a0 = v4 ? l2 + 12 : l2 + 8, an = v4 ? 8u : 32u;
         for (uint32_t w = 0; w < an; w += 2) add += bswap16(g_be16(f, a0 + w));
     }
     const uint32_t re = l4 + L;
-    uint64_t sub = (l4 & 2u) ? bswap16(g_be16(f, l4 - 2)) : 0u;
-    if (fs < re) sub += (uint64_t)f[fs] << ((fs & 1u) ? 8 : 0);
-    if (fs + 1 < re) sub += (uint64_t)f[fs + 1] << (((fs + 1) & 1u) ? 8 : 0);
+    uint32_t sub = (l4 & 2u) ? bswap16(g_be16(f, l4 - 2)) : 0u;
+    if (fs < re) sub += (uint32_t)f[fs] << ((fs & 1u) ? 8 : 0);
+    if (fs + 1 < re) sub += (uint32_t)f[fs + 1] << (((fs + 1) & 1u) ? 8 : 0);
     const uint32_t t = re - 1;
     if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
     P.st = st;
@@ -426,52 +422,43 @@ __device__ __noinline__ RPlan slow_plan(const uint8_t* f, uint32_t len) {
 
 // Masked add of one boundary chunk at frame offset o: dwords from lo4 up to byte re, plus the
 // odd-tail fix.
-DEV uint64_t masked_chunk(const uint4& v, uint32_t o, uint32_t lo4, uint32_t re, uint32_t tailfix) {
-    uint64_t a = 0;
+DEV uint32_t masked_chunk(const uint4& v, uint32_t o, uint32_t lo4, uint32_t re, uint32_t tailfix,
+                          uint32_t acc) {
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t od = o + 4u * j;
         const int nb = (int)re - (int)od;
         uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
         m = (od >= lo4) ? m : 0u;
-        a += comp(v, j) & m;
+        acc = wsum(comp(v, j) & m, acc);
     }
     const uint32_t t = re - 1;
-    if (tailfix && t >= o && t < o + 16) a += 255ull * ((comp(v, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
-    return a;
+    if (tailfix && t >= o && t < o + 16) acc += 255u * ((comp(v, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+    return acc;
 }
 
-DEV void acc_slot(uint64_t& acc, const uint4& v, uint32_t c, uint32_t lo4, uint32_t re, uint32_t tailfix) {
+DEV void acc_slot(uint32_t& acc, const uint4& v, uint32_t c, uint32_t lo4, uint32_t re, uint32_t tailfix) {
     const uint32_t o = c * 16u;
     const bool full = (o >= lo4) && (o + 16u <= re);
     const bool part = !full && (o + 16u > lo4) && (o < re);
-    if (full) acc += add_chunk(v);
-    if (part) acc += masked_chunk(v, o, lo4, re, tailfix);
+    if (full) acc = add_chunk(v, acc);
+    if (part) acc = masked_chunk(v, o, lo4, re, tailfix, acc);
 }
 
-DEV uint64_t row_sum64(uint64_t x) {  // every lane of a 16-lane row gets the row's sum
-    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-#define NFCS_DPP_STEP(ctrl)                                                              \
-    {                                                                                    \
-        uint32_t l2_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xF, 0xF, true); \
-        uint32_t h2_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xF, 0xF, true); \
-        uint64_t s_ = ((uint64_t)hi << 32 | lo) + ((uint64_t)h2_ << 32 | l2_);           \
-        lo = (uint32_t)s_;                                                               \
-        hi = (uint32_t)(s_ >> 32);                                                       \
-    }
-    NFCS_DPP_STEP(0xB1)
-    NFCS_DPP_STEP(0x4E)
-    NFCS_DPP_STEP(0x141)
-    NFCS_DPP_STEP(0x140)
-#undef NFCS_DPP_STEP
-    return ((uint64_t)hi << 32) | lo;
+template <int R>
+DEV uint32_t row_sum(uint32_t x) {  // every lane of an R-lane row gets the row's sum
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);   // quad_perm 1,0,3,2
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);   // quad_perm 2,3,0,1
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    if (R == 16) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);  // row_mirror
+    return x;
 }
 
+template <int R>
 DEV uint32_t wave_max_rows(uint32_t x) {  // x row-uniform
     uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
-    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 16));
-    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 32));
-    m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
+#pragma unroll
+    for (int l = R; l < 64; l += R) m = max(m, (uint32_t)__builtin_amdgcn_readlane((int)x, l));
     return m;
 }
 
@@ -490,17 +477,19 @@ DEV uint4 ld16(const uint4* p) {
 // descriptor array, so one wave-uniform scalar load (s_load_dwordx8) fetches all four; each
 // lane picks its row's pair. Counted on lgkmcnt, so prefetching them never holds up a vmcnt
 // wait for chunk data.
-struct Desc4 { uint32_t w[8]; };
+template <int P>  // packets per wave
+struct DescW { uint32_t w[2 * P]; };
 
-DEV Desc4 load_desc4(const nfcs_desc* __restrict__ desc, uint64_t pw, uint32_t n) {
-    Desc4 D;
-    if (pw + 4 <= n) {
+template <int P>
+DEV DescW<P> load_descw(const nfcs_desc* __restrict__ desc, uint64_t pw, uint32_t n) {
+    DescW<P> D;
+    if (pw + P <= n) {
         const uint32_t* q = (const uint32_t*)(desc + pw);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) D.w[i] = q[i];
+        for (int i = 0; i < 2 * P; ++i) D.w[i] = q[i];
     } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < P; ++i) {
             const bool ok = pw + i < n;
             D.w[2 * i] = ok ? desc[pw + i].off16 : 0u;
             D.w[2 * i + 1] = ok ? desc[pw + i].len : 0u;
@@ -509,12 +498,17 @@ DEV Desc4 load_desc4(const nfcs_desc* __restrict__ desc, uint64_t pw, uint32_t n
     return D;
 }
 
-DEV nfcs_desc pick_desc(const Desc4& D, uint32_t row) {  // mask selects: no indexable temp
-    const uint32_t m0 = 0u - (uint32_t)(row == 0), m1 = 0u - (uint32_t)(row == 1);
-    const uint32_t m2 = 0u - (uint32_t)(row == 2), m3 = 0u - (uint32_t)(row == 3);
+template <int P>
+DEV nfcs_desc pick_desc(const DescW<P>& D, uint32_t row) {  // mask selects: no indexable temp
     nfcs_desc d;
-    d.off16 = (D.w[0] & m0) | (D.w[2] & m1) | (D.w[4] & m2) | (D.w[6] & m3);
-    d.len = (D.w[1] & m0) | (D.w[3] & m1) | (D.w[5] & m2) | (D.w[7] & m3);
+    d.off16 = 0;
+    d.len = 0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const uint32_t m = 0u - (uint32_t)(row == (uint32_t)i);
+        d.off16 |= D.w[2 * i] & m;
+        d.len |= D.w[2 * i + 1] & m;
+    }
     return d;
 }
 
@@ -528,7 +522,7 @@ struct RowStage {
     uint32_t valid, bad;
 };
 
-template <int K, int NT>
+template <int K, int NT, int R = 16>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
                    uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl) {
     const bool valid = p64 < n;
@@ -546,7 +540,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t c = rl + 16u * k;
+        const uint32_t c = rl + (uint32_t)R * k;
         const uint4* a = (c < nch) ? src + c : &g_zero16;
         // NT 2: the header slot keeps the default policy so its lines are still in L2 when
         // the checksum chunks are written back; payload slots stream through as evict-first
@@ -556,7 +550,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
 // (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
-template <int K, int NT, int DBG = 0, int SM = 0>
+template <int K, int NT, int DBG = 0, int R = 16>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* patch) {
     const uint32_t len = S.len;
@@ -568,172 +562,131 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         P = rplan_none(NFCS_ST_V4_UDP);
         P.flags = F_IP | F_L4 | F_UDP; P.ipw = 24; P.rs = 34; P.re = len; P.fs = 40; P.corr = 0;
     } else {
-        P = fast_plan(S.v[0], rowbase4, len);
+        P = fast_plan<R>(S.v[0], rowbase4, len);
     }
-    if (P.st >> 8) {  // uncommon header: parsed by the row's lane 0, broadcast to the row
-        RPlan Q = rplan_none(0);
-        if (rl == 0) Q = slow_plan(frame, len);
-        P.st = row_bcast<0>(Q.st);
-        P.flags = row_bcast<0>(Q.flags);
-        P.ipw = row_bcast<0>(Q.ipw);
-        P.rs = row_bcast<0>(Q.rs);
-        P.re = row_bcast<0>(Q.re);
-        P.fs = row_bcast<0>(Q.fs);
-        P.corr = ((uint64_t)row_bcast<0>((uint32_t)(Q.corr >> 32)) << 32) | row_bcast<0>((uint32_t)Q.corr);
-    }
-    if (!S.valid || S.bad) P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
+    const bool live = S.valid && !S.bad;
+    // uncommon headers (IP options, IHL < 5, IHL past the frame) take the cold path below,
+    // after the chunk registers are dead, so it adds nothing to the kernel's register peak
+    const bool slow = live && (P.st >> 8) != 0;
+    if (!live || slow) P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
     uint32_t st = P.st;
     uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
     uint32_t l4w = NFCS_PATCH_NONE;
-    if (P.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation on lane 0
-        SeqOut o = {0, 0, 0, 0, 0};
-        if (rl == 0) o = seq_update(frame, len);
-        st = row_bcast<0>(o.st) | NFCS_ST_FLAG_OVERLAP;
-        ipw = row_bcast<0>((o.ip_off & 0xFFFFu) | (o.ip_val << 16));
-        l4w = row_bcast<0>((o.l4_off & 0xFFFFu) | (o.l4_val << 16));
-    }
     // region sums (rows without an L4 region add nothing). rlv is opaque so the per-slot
     // offsets are recomputed rather than hoisted into ~35 long-lived VGPRs.
     const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
     const uint32_t tailfix = P.flags & F_TAIL;
     uint32_t rlv = rl;
     asm volatile("" : "+v"(rlv));
-    uint64_t acc = 0;
+    uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc_slot(acc, S.v[k], rlv + 16u * k, lo4, re, tailfix);
-    // continuation batches for frames longer than 16*K chunks (jumbo)
+    for (int k = 0; k < K; ++k) acc_slot(acc, S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
+    // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t nre = (re + 15u) >> 4;
-    const uint32_t cmax = wave_max_rows(nre);
-    for (uint32_t cb = 16u * K; cb < cmax; cb += 16u * K) {
+    const uint32_t cmax = wave_max_rows<R>(nre);
+    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
         uint4 w[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t c = cb + rlv + 16u * k;
+            const uint32_t c = cb + rlv + (uint32_t)R * k;
             w[k] = ld16<NT>((c < nre) ? src + c : &g_zero16);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + 16u * k, lo4, re, tailfix);
+        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k, lo4, re, tailfix);
     }
-    const uint64_t z = row_sum64(acc) + P.corr;
+    const uint32_t z = row_sum<R>(acc) + P.corr;
     if (P.flags & F_L4) {
-        uint32_t c = (~fold64(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
+        uint32_t c = (~fold32(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
         if ((P.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
         l4w = P.fs | (c << 16);
     }
-    // Write back the (at most 4) checksum bytes.
-    //  SM 0: byte stores from lanes 0..3.
-    //  SM 1: each lane whose header chunk holds a field byte rewrites its whole 16-byte chunk
-    //        from registers with the new bytes merged (frames start on 16-byte boundaries, so a
-    //        chunk never holds another frame's bytes): full-sector writes, no partial lines.
-    //  SM 3: as 1, the whole first 128-byte line when the frame owns it; SM 4: field dwords
-    //  SM 5/6/7: as 1/4/3 with the chunk re-loaded right before the store.
-    if (!(DBG & 1) && !(P.flags & F_SEQ)) {
-        if (SM == 0) {
-            if (rl < 4) {
-                const uint32_t w = (rl & 2u) ? l4w : ipw;
-                const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-                if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
-            }
-        } else if (rl < 8) {
-            // field bytes that fall into this lane's header chunk (data independent)
-            const uint32_t offs[2] = {ipw & 0xFFFFu, l4w & 0xFFFFu};
-            const uint32_t vals[2] = {ipw >> 16, l4w >> 16};
-            uint32_t keep[4] = {~0u, ~0u, ~0u, ~0u}, put[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int f = 0; f < 2; ++f) {
-#pragma unroll
-                for (uint32_t bb = 0; bb < 2; ++bb) {
-                    const uint32_t pos = offs[f] + bb;
-                    const bool mine = offs[f] != NFCS_PATCH_NONE && (pos >> 4) == rl;
-                    const uint32_t j = (pos >> 2) & 3u, sh = 8u * (pos & 3u);
-                    const uint32_t val = (vals[f] >> (8 * bb)) & 0xFFu;
-#pragma unroll
-                    for (uint32_t q = 0; q < 4; ++q) {
-                        const bool hit = mine && j == q;
-                        keep[q] &= hit ? ~(0xFFu << sh) : ~0u;
-                        put[q] |= hit ? (val << sh) : 0u;
-                    }
-                }
-            }
-            const uint32_t tm = (keep[0] != ~0u ? 1u : 0u) | (keep[1] != ~0u ? 2u : 0u) |
-                                (keep[2] != ~0u ? 4u : 0u) | (keep[3] != ~0u ? 8u : 0u);
-            // SM 3/7: the whole first L2 line (every field lies in bytes < 128) when the frame
-            // owns it; SM 5/6/7 re-load the chunk just before the store so the store finds its
-            // line in L2 (a store to a line not in L2 stalls the read stream, profiles/)
-            const bool line = (SM == 3 || SM == 7) && (((uintptr_t)frame & 127u) == 0) && len >= 128u;
-            const bool st16 = line || tm != 0;
-            uint4 c = S.v[0];
-            if (SM >= 5 && st16) {
-                c = ld16<0>((const uint4*)frame + rl);
-            }
-            c.x = (c.x & keep[0]) | put[0];
-            c.y = (c.y & keep[1]) | put[1];
-            c.z = (c.z & keep[2]) | put[2];
-            c.w = (c.w & keep[3]) | put[3];
-            if (SM == 4 || SM == 6) {  // only the dwords that hold field bytes
-                uint32_t* q = (uint32_t*)((uint4*)frame + rl);
-                if (tm & 1u) q[0] = c.x;
-                if (tm & 2u) q[1] = c.y;
-                if (tm & 4u) q[2] = c.z;
-                if (tm & 8u) q[3] = c.w;
-            } else if (st16) {
-                ((uint4*)frame)[rl] = c;
+    // Write back the (at most 4) checksum bytes from lanes 0..3 of the row (byte stores
+    // measured fastest: chunk, dword, whole-line and re-load-then-store write-backs all
+    // slower), then the status byte / patch record from lane 0.
+    auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool frame_stores) {
+        if (!(DBG & 1) && frame_stores && on && rl < 4) {
+            const uint32_t w = (rl & 2u) ? l4w_ : ipw_;
+            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+        }
+        if (on && rl == 0) {
+            if (status) status[S.p] = (uint8_t)st_;
+            if (patch) {
+                uint2 r;
+                r.x = (ipw_ & 0xFFFFu) | (l4w_ << 16);
+                r.y = (ipw_ >> 16) | (l4w_ & 0xFFFF0000u);
+                ((uint2*)patch)[S.p] = r;
             }
         }
-    }
+    };
+    emit(S.valid && !slow, st, ipw, l4w, true);
     if (DBG & 4) __builtin_amdgcn_s_setprio(0);
-    if (S.valid && rl == 0) {
-        if (status) status[S.p] = (uint8_t)st;
-        if (patch) {
-            uint2 r;
-            r.x = (ipw & 0xFFFFu) | (l4w << 16);
-            r.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
-            ((uint2*)patch)[S.p] = r;
+    if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
+        // Uncommon headers, handled last so that only the frame address and length are live
+        // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
+        // exact sequential emulation, which writes its own bytes) and the region is re-summed
+        // from memory.
+        RPlan Q = rplan_none(0);
+        SeqOut o = {0, 0, 0, 0, 0};
+        if (slow && rl == 0) {
+            Q = slow_plan(frame, len);
+            if (Q.flags & F_SEQ) o = seq_update(frame, len);
         }
+        Q.st = row_bcast<0, R>(Q.st);
+        Q.flags = row_bcast<0, R>(Q.flags);
+        Q.ipw = row_bcast<0, R>(Q.ipw);
+        Q.rs = row_bcast<0, R>(Q.rs);
+        Q.re = row_bcast<0, R>(Q.re);
+        Q.fs = row_bcast<0, R>(Q.fs);
+        Q.corr = row_bcast<0, R>(Q.corr);
+        const uint32_t ost = row_bcast<0, R>(o.st);
+        const uint32_t oip = row_bcast<0, R>((o.ip_off & 0xFFFFu) | (o.ip_val << 16));
+        const uint32_t ol4 = row_bcast<0, R>((o.l4_off & 0xFFFFu) | (o.l4_val << 16));
+        const bool seq = slow && (Q.flags & F_SEQ);
+        const uint32_t re2 = (slow && !seq && (Q.flags & F_L4)) ? Q.re : 0u;
+        const uint32_t lo42 = Q.rs & ~3u, tf2 = Q.flags & F_TAIL;
+        uint32_t acc2 = 0;
+        for (uint32_t c = rl; c < ((re2 + 15u) >> 4); c += R) acc_slot(acc2, src[c], c, lo42, re2, tf2);
+        const uint32_t z2 = row_sum<R>(acc2) + Q.corr;
+        uint32_t st2 = Q.st, ipw2 = (Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE, l4w2 = NFCS_PATCH_NONE;
+        if (Q.flags & F_L4) {
+            uint32_t c = (~fold32(z2)) & 0xFFFFu;
+            if ((Q.flags & F_UDP) && c == 0) c = 0xFFFFu;
+            l4w2 = Q.fs | (c << 16);
+        }
+        if (seq) {
+            st2 = ost | NFCS_ST_FLAG_OVERLAP;
+            ipw2 = oip;
+            l4w2 = ol4;
+        }
+        emit(slow, st2, ipw2, l4w2, !seq);
     }
 }
 
-// Grid-stride over packets, 16 rows (packets) per 256-thread block. PIPE: the next packet's
-// first batch is issued before the current one is processed (two stages of K slots live).
-template <int K, int NT, bool PIPE, int DBG = 0, int SM = 0, int OCC = 1>
+// Grid-stride over packets (the default grid has one workgroup per 4*64/R packets, so no
+// loop), 64/R packet rows per wave.
+template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1>
 __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
-                                                             uint64_t arena_bytes,
-                                                             const nfcs_desc* __restrict__ desc,
-                                                             uint32_t n, uint32_t base16,
-                                                             uint8_t* __restrict__ status,
-                                                             nfcs_patch* __restrict__ patch) {
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
-    const uint32_t rowbase4 = (lane & ~15u) * 4u;
-    const uint32_t stride = gridDim.x * (kBlock / 16);
-    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / 16) + rfl(threadIdx.x >> 6) * 4u;
+                                                                  uint64_t arena_bytes,
+                                                                  const nfcs_desc* __restrict__ desc,
+                                                                  uint32_t n, uint32_t base16,
+                                                                  uint8_t* __restrict__ status,
+                                                                  nfcs_patch* __restrict__ patch) {
+    constexpr uint32_t PW = 64 / R;  // packets per wave
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint32_t stride = gridDim.x * (kBlock / R);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
     if (w0 >= n) return;
-    if (!PIPE) {
-        Desc4 Dn = load_desc4(desc, w0, n);
-        for (uint64_t pw = w0; pw < n; pw += stride) {
-            const Desc4 D = Dn;
-            if (pw + stride < n) Dn = load_desc4(desc, pw + stride, n);  // prefetch (lgkmcnt)
-            RowStage<K> S;
-            if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
-            row_stage<K, NT>(S, arena, arena_bytes, pick_desc(D, row), pw + row, n, base16, rl);
-            if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-            row_process<K, NT, DBG, SM>(S, rl, rowbase4, status, patch);
-        }
-    } else {
-        RowStage<K> A;
-        row_stage<K, NT>(A, arena, arena_bytes, pick_desc(load_desc4(desc, w0, n), row), w0 + row,
-                         n, base16, rl);
-        Desc4 Dn = load_desc4(desc, w0 + stride < n ? w0 + stride : w0, n);
-        for (uint64_t pw = w0; pw < n; pw += stride) {
-            const uint64_t pn = pw + stride;
-            const bool more = pn < n;
-            const Desc4 D = Dn;
-            if (pn + stride < n) Dn = load_desc4(desc, pn + stride, n);
-            RowStage<K> B;  // always staged (a re-read of p at the end) so waits stay counted
-            row_stage<K, NT>(B, arena, arena_bytes, pick_desc(D, row), (more ? pn : pw) + row, n,
-                             base16, rl);
-            row_process<K, NT, DBG, SM>(A, rl, rowbase4, status, patch);
-            A = B;
-        }
+    DescW<PW> Dn = load_descw<PW>(desc, w0, n);
+    for (uint64_t pw = w0; pw < n; pw += stride) {
+        const DescW<PW> D = Dn;
+        if (pw + stride < n) Dn = load_descw<PW>(desc, pw + stride, n);  // prefetch (lgkmcnt)
+        RowStage<K> S;
+        if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
+        row_stage<K, NT, R>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl);
+        if (DBG & 8) __builtin_amdgcn_s_setprio(0);
+        row_process<K, NT, DBG, R>(S, rl, rowbase4, status, patch);
     }
 }
 
@@ -751,7 +704,7 @@ DEV uint32_t q_take(uint32_t* q, uint32_t x) {  // lane 0 takes a unit; result s
     return v;
 }
 
-template <int K, int NT, int DBG = 0, int SM = 0>
+template <int K, int NT, int R = 16, int DBG = 0>
 __global__ __launch_bounds__(kBlock) void update_queue_kernel(uint8_t* __restrict__ arena,
                                                               uint64_t arena_bytes,
                                                               const nfcs_desc* __restrict__ desc,
@@ -759,9 +712,10 @@ __global__ __launch_bounds__(kBlock) void update_queue_kernel(uint8_t* __restric
                                                               uint8_t* __restrict__ status,
                                                               nfcs_patch* __restrict__ patch,
                                                               uint32_t* __restrict__ q) {
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
-    const uint32_t rowbase4 = (lane & ~15u) * 4u;
-    const uint32_t units = (n + 3u) >> 2;
+    constexpr uint32_t PW = 64 / R;  // packets per wave (one unit)
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint32_t units = (n + PW - 1) / PW;
     const uint32_t per = (units + 7u) >> 3;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     auto cnt = [&](uint32_t x) -> uint32_t {
@@ -780,19 +734,19 @@ __global__ __launch_bounds__(kBlock) void update_queue_kernel(uint8_t* __restric
     };
     uint32_t cur = take_next(rfl(q_take(q, x)));
     if (cur != kNone) {
-        Desc4 D = load_desc4(desc, (uint64_t)cur * 4u, n);
+        DescW<PW> D = load_descw<PW>(desc, (uint64_t)cur * PW, n);
         uint32_t pend = q_take(q, x);
         for (;;) {
-            const uint64_t pw = (uint64_t)cur * 4u;
+            const uint64_t pw = (uint64_t)cur * PW;
             RowStage<K> S;
-            row_stage<K, NT>(S, arena, arena_bytes, pick_desc(D, row), pw + row, n, base16, rl);
+            row_stage<K, NT, R>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl);
             const uint32_t nxt = take_next(rfl(pend));  // counted wait: the frames stay in flight
-            Desc4 Dn = D;
+            DescW<PW> Dn = D;
             if (nxt != kNone) {
-                Dn = load_desc4(desc, (uint64_t)nxt * 4u, n);
+                Dn = load_descw<PW>(desc, (uint64_t)nxt * PW, n);
                 pend = q_take(q, x);
             }
-            row_process<K, NT, DBG, SM>(S, rl, rowbase4, status, patch);
+            row_process<K, NT, DBG, R>(S, rl, rowbase4, status, patch);
             if (nxt == kNone) break;
             cur = nxt;
             D = Dn;
@@ -841,31 +795,36 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                          const Work& work) {
     nfcs_patch* ws = work.patch;
     if (n == 0) return hipSuccess;
-    // One 16-packet block per 256-thread workgroup, as many workgroups as blocks (a grid
-    // that grid-strides over resident workgroups measured 10-15% slower: profiles/).
-    const uint32_t blocks_need = (n + 15u) / 16u;
-    const int g = grid > 0 ? (grid < (int)blocks_need ? grid : (int)blocks_need) : (int)blocks_need;
-#define NFCS_ROWSO(K, NT, PIPE, DBG, SM, OCC, PP)                                                \
-    hipLaunchKernelGGL((update_rows_kernel<K, NT, PIPE, DBG, SM, OCC>), dim3(g), dim3(kBlock), 0, \
-                       stream, arena, arena_bytes, desc, n, base16, status, PP)
-#define NFCS_ROWSP(K, NT, PIPE, DBG, SM, PP) NFCS_ROWSO(K, NT, PIPE, DBG, SM, 1, PP)
-    // work-queue form: resident grid (5 waves per SIMD at this kernel's register count)
+    // One workgroup per 4*64/R packets, as many workgroups as that takes (a grid that
+    // grid-strides over resident workgroups measured 10-15% slower: DESIGN.md §5).
+    auto rows_grid = [&](int R) {
+        const uint32_t per_block = (uint32_t)(kBlock / R);
+        const uint32_t need = (n + per_block - 1) / per_block;
+        return grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
+    };
+#define NFCS_ROWSO(K, NT, R, DBG, OCC, PP)                                                       \
+    hipLaunchKernelGGL((update_rows_kernel<K, NT, R, DBG, OCC>), dim3(rows_grid(R)), dim3(kBlock), \
+                       0, stream, arena, arena_bytes, desc, n, base16, status, PP)
+#define NFCS_ROWSP(K, NT, R, DBG, PP) NFCS_ROWSO(K, NT, R, DBG, 1, PP)
+#define NFCS_ROWS(K, NT, R) NFCS_ROWSP(K, NT, R, 0, patch)
+    // work-queue form: a resident grid (5 waves per SIMD at this kernel's register count)
     const int gq = grid > 0 ? grid : di.cus * 5;
-#define NFCS_QUEUE(K, NT, DBG, SM)                                                              \
-    hipLaunchKernelGGL((update_queue_kernel<K, NT, DBG, SM>), dim3(gq), dim3(kBlock), 0, stream, \
+#define NFCS_QUEUE(K, NT, R, DBG)                                                                \
+    hipLaunchKernelGGL((update_queue_kernel<K, NT, R, DBG>), dim3(gq), dim3(kBlock), 0, stream,  \
                        arena, arena_bytes, desc, n, base16, status, patch, work.queue)
-#define NFCS_ROWS(K, NT, PIPE) NFCS_ROWSP(K, NT, PIPE, 0, 0, patch)
     switch (variant) {
     default:
-    case 0: NFCS_ROWS(6, 2, false); break;  // header slot cached, payload slots evict-first
-    case 1: NFCS_ROWS(6, 0, false); break;  // all loads default policy
-    case 2: NFCS_ROWS(4, 2, false); break;
-    case 3: NFCS_ROWS(6, 2, true); break;   // next packet's batch issued before processing
-    case 4: NFCS_ROWS(6, 1, false); break;  // all loads evict-first
+    case 0: NFCS_ROWS(6, 2, 16); break;   // 16-lane rows; header slot cached, payload evict-first
+    case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
+    case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
+    case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
+    case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
+    case 6: NFCS_QUEUE(6, 2, 16, 0); break;   // work queue, 16-lane rows
+    case 7: NFCS_QUEUE(12, 2, 8, 0); break;   // work queue, 8-lane rows
     case 8: {  // split: checksum pass without frame stores, then the patch pass
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
-        NFCS_ROWSP(6, 2, false, 1, 0, pp);
+        NFCS_ROWSP(6, 2, 16, 1, pp);
         int ga = (int)((n + kBlock - 1) / kBlock);
         if (ga > di.cus * 8) ga = di.cus * 8;
         hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
@@ -873,26 +832,18 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         break;
     }
 #ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
-    case 101: NFCS_ROWSP(6, 2, false, 1, 0, patch); break;  // no frame stores
-    case 102: NFCS_ROWSP(6, 2, false, 2, 0, patch); break;  // no parse (fixed C1 plan)
-    case 103: NFCS_ROWSP(6, 2, false, 3, 0, patch); break;  // neither
-    case 121: NFCS_ROWSP(6, 2, false, 0, 1, patch); break;  // 16-byte chunk write-back
-    case 123: NFCS_ROWSP(6, 2, false, 0, 3, patch); break;  // 128-byte header line write-back
-    case 124: NFCS_ROWSP(6, 2, false, 0, 4, patch); break;  // field dwords only
-    case 125: NFCS_ROWSP(6, 1, false, 0, 3, patch); break;  // 123 with all loads nt
-    case 126: NFCS_ROWSP(6, 0, false, 0, 3, patch); break;  // 123 with all loads default
-    case 127: NFCS_ROWSP(6, 2, false, 0, 5, patch); break;  // re-load + 16-byte chunk store
-    case 128: NFCS_ROWSP(6, 2, false, 0, 6, patch); break;  // re-load + field dword stores
-    case 129: NFCS_ROWSP(6, 2, false, 0, 7, patch); break;  // re-load + 128-byte line store
-    case 150: NFCS_QUEUE(6, 2, 0, 0); break;   // work queue
-    case 151: NFCS_QUEUE(6, 2, 1, 0); break;   // work queue, no frame stores
-    case 152: NFCS_QUEUE(6, 2, 4, 0); break;   // work queue, high priority compute phase
-    case 141: NFCS_ROWSP(6, 2, false, 4, 0, patch); break;  // high priority compute phase
-    case 142: NFCS_ROWSP(6, 2, false, 8, 0, patch); break;  // high priority load issue
-    case 143: NFCS_ROWSP(6, 2, false, 4, 4, patch); break;  // 141 + field dword stores
-    case 131: NFCS_ROWSO(6, 2, false, 0, 0, 6, patch); break;  // >= 6 waves per SIMD
-    case 132: NFCS_ROWSO(6, 2, false, 0, 0, 8, patch); break;  // >= 8 waves per SIMD
-    case 133: NFCS_ROWSO(6, 2, false, 0, 3, 8, patch); break;  // 132 + line write-back
+    case 101: NFCS_ROWSP(6, 2, 16, 1, patch); break;  // no frame stores
+    case 102: NFCS_ROWSP(6, 2, 16, 2, patch); break;  // no parse (fixed C1 plan)
+    case 103: NFCS_ROWSP(6, 2, 16, 3, patch); break;  // neither
+    case 105: NFCS_ROWSP(12, 2, 8, 1, patch); break;  // 8-lane rows, no frame stores
+    case 106: NFCS_ROWSP(12, 2, 8, 3, patch); break;  // 8-lane rows, no stores, no parse
+    case 131: NFCS_ROWSO(6, 2, 16, 0, 6, patch); break;  // >= 6 waves per SIMD
+    case 141: NFCS_ROWSP(6, 2, 16, 4, patch); break;  // high priority compute phase
+    case 142: NFCS_ROWSP(6, 2, 16, 8, patch); break;  // high priority load issue
+    case 151: NFCS_QUEUE(6, 2, 16, 1); break;  // work queue, no frame stores
+    case 152: NFCS_QUEUE(6, 2, 16, 4); break;  // work queue, high priority compute phase
+    case 155: NFCS_ROWS(12, 1, 8); break;      // 8-lane rows, all loads evict-first
+    case 156: NFCS_ROWS(8, 2, 8); break;       // 8-lane rows, 8 slots
 #endif
     }
 #undef NFCS_ROWS
