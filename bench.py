@@ -240,7 +240,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u16 one's-complement (u8 frames, u64 accumulate)",
+        "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
         "config": {"workload": WORKLOAD[args.config], "packets_per_gpu": n, "frame_align": args.align,
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},

@@ -50,8 +50,9 @@ namespace {
 
 thread_local int g_last_hip = 0;
 
-hipError_t ensure_ws(nfcs_ctx* c, size_t n) {
-    if (!nfcs::variant_needs_ws(c->variant) || n <= c->ws_cap) return hipSuccess;
+hipError_t ensure_ws(nfcs_ctx* c, size_t n, uint64_t arena_bytes) {
+    if (!nfcs::variant_needs_ws(c->variant, arena_bytes, (uint32_t)n) || n <= c->ws_cap)
+        return hipSuccess;
     if (c->ws) (void)hipFree(c->ws);
     c->ws = nullptr;
     c->ws_cap = 0;
@@ -203,7 +204,7 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
     if (!c) return NFCS_EINVAL;
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
-    NFCS_HIP(ensure_ws(c, n));
+    NFCS_HIP(ensure_ws(c, n, arena_bytes));
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
                                  pick(c, stream), c->variant, c->grid, c->work(n)));
     return NFCS_OK;
@@ -394,7 +395,7 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
                                      int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0) return NFCS_EINVAL;
     hipStream_t st = pick(c, stream);
-    NFCS_HIP(ensure_ws(c, n));
+    NFCS_HIP(ensure_ws(c, n, arena_bytes));
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,

@@ -40,8 +40,18 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                          nfcs_patch* patch, hipStream_t stream, int variant, int grid,
                          const Work& work);
 
+// Split mode (checksum pass without frame stores, then a patch-apply pass) beats the fused
+// kernel once frames are large: a store in the middle of a long read stream costs more than
+// the same store in its own pass. The default variant picks it when the mean
+// arena footprint per packet is at least kSplitMeanBytes.
+constexpr uint64_t kSplitMeanBytes = 2048;
+inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
+    return variant == 8 || (variant == 0 && n > 0 && arena_bytes / n >= kSplitMeanBytes);
+}
 // variants that stage patch records in a context workspace (split mode)
-inline bool variant_needs_ws(int variant) { return variant == 8; }
+inline bool variant_needs_ws(int variant, uint64_t arena_bytes, uint32_t n) {
+    return use_split(variant, arena_bytes, n);
+}
 
 hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint64_t first,
                              uint32_t n, uint8_t* arena, uint64_t arena_bytes,

@@ -812,6 +812,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 #define NFCS_QUEUE(K, NT, R, DBG)                                                                \
     hipLaunchKernelGGL((update_queue_kernel<K, NT, R, DBG>), dim3(gq), dim3(kBlock), 0, stream,  \
                        arena, arena_bytes, desc, n, base16, status, patch, work.queue)
+    if (use_split(variant, arena_bytes, n)) variant = 8;
     switch (variant) {
     default:
     case 0: NFCS_ROWS(6, 2, 16); break;   // 16-lane rows; header slot cached, payload evict-first

@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC counter passes for the checksum kernel (one counter group per rocprofv3 run, kernel-trace
 # only, never combined with sys/runtime tracing). Usage: tools/pmc.sh <outdir> <bench args...>
+# PMC_GROUPS="A B;C;D E" overrides the default groups (one rocprofv3 pass per group).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out/$1; shift
@@ -15,11 +16,12 @@ while read -r group; do
       python3 bench.py "$@" --no-cpu > "$OUT/pmc$i.log" 2>&1
   rc=$?; echo "pmc pass $i ($group) rc=$rc"
   if fatal $rc; then exit $rc; fi
-done <<'GROUPS'
+done < <(if [ -n "${PMC_GROUPS:-}" ]; then echo "$PMC_GROUPS" | tr ';' '\n'; else cat <<'GROUPS'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY
 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE
 FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
 GROUPS
+fi)
 exit 0

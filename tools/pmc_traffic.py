@@ -24,25 +24,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 
 
-def run_pass(out, cfg, counter, steps):
-    d = os.path.join(out, f"c{cfg}_{counter}")
-    cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d,
+def run_pass(out, cfg, counters, steps):
+    """One rocprofv3 pass with the given counters; median per counter over update launches."""
+    d = os.path.join(out, f"c{cfg}_{counters[0]}")
+    cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--no-cpu"]
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu"]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 failed ({r.returncode}): {r.stderr[-2000:]}")
-    vals = []
+    vals = {c: [] for c in counters}
     for root, _, files in os.walk(d):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for row in csv.DictReader(open(os.path.join(root, f))):
-                    if "update_rows_kernel" in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                        vals.append(float(row["Counter_Value"]))
-    if not vals:
-        raise SystemExit(f"no {counter} samples for the update kernel in {d}")
-    return statistics.median(vals), len(vals)
+                    if "update_rows_kernel" in row["Kernel_Name"] and row["Counter_Name"] in vals:
+                        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for c, v in vals.items():
+        if not v:
+            raise SystemExit(f"no {c} samples for the update kernel in {d}")
+    return {c: statistics.median(v) for c, v in vals.items()}, min(len(v) for v in vals.values())
 
 
 def main():
@@ -51,17 +53,29 @@ def main():
     ap.add_argument("--configs", type=int, nargs="+", default=[1, 2, 3])
     ap.add_argument("--steps", type=int, default=5)
     a = ap.parse_args()
+    a.out = os.path.abspath(a.out)  # rocprofv3 runs with cwd /tmp
     os.makedirs(a.out, exist_ok=True)
-    res = {"method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, --kernel-trace; "
-                     "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 correction), write = WRITE_SIZE x 1024; "
-                     "median over launches of bench.py"}
+    res = {"method": "rocprofv3 --pmc, --kernel-trace only, separate passes; read bytes = "
+                     "2 x FETCH_SIZE x 1024 (gfx950 correction), write = WRITE_SIZE x 1024; "
+                     "cross-check: TCC_EA0_RDREQ x 128 B (gfx950 read requests are whole 128-B "
+                     "lines; the stock 64-B expression under-counts by the same factor 2), "
+                     "EA0_WRREQ(_64B) write requests; median over launches of bench.py"}
     for cfg in a.configs:
-        f, nf_ = run_pass(a.out, cfg, "FETCH_SIZE", a.steps)
-        w, nw = run_pass(a.out, cfg, "WRITE_SIZE", a.steps)
-        fb, wb = 2 * f * 1024, w * 1024
+        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps)
+        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps)
+        q, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
+                        a.steps)
+        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps)
+        fb, wb = 2 * f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
+        rq = q["TCC_EA0_RDREQ_sum"]
+        rb_req = rq * 128
         res[f"C{cfg}"] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
-                          "per_packet": (fb + wb) / PACKETS[cfg], "launches": min(nf_, nw)}
-        print(f"C{cfg}: read {fb / 1e9:.3f} GB  write {wb / 1e6:.1f} MB per launch", flush=True)
+                          "per_packet": (fb + wb) / PACKETS[cfg], "launches": min(nf_, nw),
+                          "read_bytes_from_requests": rb_req, "read_requests": rq,
+                          "write_requests": wq["TCC_EA0_WRREQ_sum"],
+                          "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}
+        print(f"C{cfg}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
+              f"{wb / 1e6:.1f} MB in {wq['TCC_EA0_WRREQ_sum']:.0f} requests per launch", flush=True)
     with open(os.path.join(a.out, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
 

@@ -18,8 +18,12 @@ __global__ __launch_bounds__(256) void rw(uint4* __restrict__ p, size_t n16, uns
     const size_t stride = (size_t)gridDim.x * 256;
     uint64_t acc = 0;
     for (; i < n16; i += stride) {
-        const uint4 v = p[i];
-        acc += (uint64_t)v.x + v.y + v.z + v.w;
+        const uint4 v0 = p[i];
+        acc += (uint64_t)v0.x + v0.y + v0.z + v0.w;
+        // opaque copy: a store of the just-loaded value back to its own address is otherwise
+        // removed as a dead store by the compiler (an earlier version measured exactly that)
+        uint4 v = v0;
+        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
         const uint32_t c = (uint32_t)(i % 96);  // chunk within the 1536-B frame
         if (MODE == 1 && c == 1) ((uint8_t*)(p + i))[8] = (uint8_t)v.z;
         if (MODE == 2 && c == 1) ((uint8_t*)(p + i))[8] = (uint8_t)v.z;
