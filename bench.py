@@ -9,6 +9,10 @@ so per-GPU work is fixed (weak scaling) and there is no collective on the data p
 only meet at the timing barriers.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1] [--packets n] [--no-cpu]
+                  [--op update|l3fwd]
+
+--op l3fwd measures the fused transit-IPv4 forward instead (TTL--, MAC rewrite,
+update_checksums; nfcs_l3_forward_device) on C1 with next hop i % 9 (8 = no route).
 
 Prints ONE JSON line on rank 0. `value` = sum over ranks of frame bytes per step / the max
 over ranks of the timed wall time per step. `roofline` uses the kernel's HIP-event time on its
@@ -120,7 +124,15 @@ def golden_digest(config: int, first: int, n: int):
     return None
 
 
-def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0):
+def golden_l3():
+    try:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+    except OSError:
+        return None
+    return g.get("l3fwd_c1")
+
+
+def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str = "update"):
     """Reference update_checksums() on host cores over a bounded sample of the workload."""
     try:
         import oracle
@@ -131,7 +143,22 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0):
     n = {0: 1024, 1: 1 << 20, 2: 1 << 17, 3: 1 << 21}[config]
     arena, desc = oracle.gen_config(config, SEED, 0, n)
     nbytes = float(desc["len"].astype(np.float64).sum())
-    if kind == "reference":
+    if op == "l3fwd":
+        g = golden_l3()
+        table = np.frombuffer(bytes.fromhex(g["table"]), dtype=np.uint8).copy()
+        nh = (np.arange(n) % 9).astype(np.uint32)
+        if kind == "reference":
+            R = oracle.ref()
+            run = lambda: R.nfref_l3_forward_batch(oracle._ptr(arena), desc.ctypes.data,
+                                                   oracle._ptr(nh, oracle._u32p), n,
+                                                   oracle._ptr(table), 8, threads)
+        else:
+            L = oracle.lib()
+            run = lambda: L.nfo_l3_forward_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data,
+                                                 oracle._ptr(nh, oracle._u32p), n,
+                                                 oracle._ptr(table), 8, None)
+            threads = 1
+    elif kind == "reference":
         R = oracle.ref()
         run = lambda: R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, n, threads)
     else:
@@ -178,6 +205,7 @@ def main():
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--op", choices=["update", "l3fwd"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -191,17 +219,34 @@ def main():
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n, args.align)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
+    l3 = args.op == "l3fwd"
+    if l3:
+        # every launch decrements TTL (64 in the generator): K + 1 launches per fresh batch
+        if args.steps > 60:
+            raise SystemExit("--op l3fwd: --steps <= 60 (TTL 64 runs out after 63 forwards)")
+        g3 = golden_l3()
+        table = np.frombuffer(bytes.fromhex(g3["table"]), dtype=np.uint8).copy()
+        d_tab = eng.alloc(table.nbytes).upload(table)
+        d_nh = eng.alloc(4 * n).upload(((np.arange(first, first + n)) % 9).astype(np.uint32))
+        algo_bytes = frame_bytes + 37.0 * n  # + 4 csum + 12 MAC + 1 TTL written, 8 desc + 4 nh + 8 table read
+        step = lambda: eng.l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8)
+        regen = lambda: (eng.gen_config_device(args.config, SEED, first, n, d_arena, nbytes, d_desc),
+                         eng.sync())
+    else:
+        step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
+        regen = lambda: None
 
     # untimed warm-up: W steps, continued until --warm-seconds have passed so the timed steps
     # run at the clock the GPU holds under this load (a cold start measured ~4% slower)
     tw = time.perf_counter()
     done = 0
     while done < args.warmup or time.perf_counter() - tw < args.warm_seconds:
-        eng.update_device(d_arena, nbytes, d_desc, n)
+        step()
         done += 1
         if done % 16 == 0:
             eng.sync()
     eng.sync()
+    regen()  # l3fwd: fresh TTLs for the timed steps
 
     # timed region: barrier + device sync on both sides, max over ranks
     D.barrier()
@@ -209,7 +254,7 @@ def main():
     eng.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.update_device(d_arena, nbytes, d_desc, n)
+        step()
     eng.sync()
     device_sync()
     t1 = time.perf_counter()
@@ -219,18 +264,28 @@ def main():
     total_frame_bytes = D.sum(frame_bytes)
 
     # kernel duration with HIP events on the launch stream (roofline), same launches
-    ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
+    if l3:
+        regen()
+        ev_ms = eng.time_l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8,
+                                           args.steps) / args.steps
+        # parity: one forward of a fresh batch vs the reference's digest (C1, rank 0 shard)
+        regen()
+        step()
+        eng.sync()
+        want = g3["digest_out"] if (args.config == 1 and first == 0 and n == g3["n"]) else None
+    else:
+        ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
+        # parity of what was measured: digest of the updated arena vs the reference's
+        want = golden_digest(args.config, first, n)
     achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
-
-    # parity of what was measured: digest of the updated arena vs the reference's
-    want = golden_digest(args.config, first, n)
     got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
     parity_ok = None if want is None else (got == want)
     parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    traffic = load_traffic(args.config, n)
+    traffic = None if l3 else load_traffic(args.config, n)
     out = {
-        "metric": "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X",
+        "metric": "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X"
+                  + (" (fused L3 forward: TTL--, MAC rewrite, checksums)" if l3 else ""),
         "value": round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
         "unit": "GB/s",
         "n_gpus": ws,
@@ -242,7 +297,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
-        "config": {"workload": WORKLOAD[args.config], "packets_per_gpu": n, "frame_align": args.align,
+        "config": {"workload": WORKLOAD[args.config] + (", fused L3 forward (next hop i % 9)" if l3 else ""),
+                   "packets_per_gpu": n, "frame_align": args.align,
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -254,7 +310,7 @@ def main():
         "parity": {"digest": got, "reference_digest": want, "match": parity_ok, "all_ranks": parity_all},
     }
     if rank == 0 and ws == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -73,11 +73,17 @@ enum {
     NFCS_ST_V6_TCP = 7,     /* IPv6 TCP checksum                                                     */
     NFCS_ST_V6_UDP = 8,     /* IPv6 UDP checksum                                                     */
     NFCS_ST_V6_L4SKIP = 9,  /* IPv6 TCP/UDP branch returned early (bounds): untouched                */
+    /* nfcs_l3_forward_device only (switch.hpp:247-294); such frames are left untouched:    */
+    NFCS_ST_NO_ROUTE = 11,  /* next-hop index >= table size: no route / ARP miss (282-294)       */
+    NFCS_ST_NOT_IPV4 = 12,  /* L3 EtherType (after one tag) not IPv4, or ipv4() absent (265-267) */
+    NFCS_ST_TTL_EXPIRED = 13, /* TTL <= 1: the switch sends ICMP time exceeded and drops (278)   */
     NFCS_ST_OOB = 14,       /* IPv4 with l2 + IHL*4 > len: the reference reads past the frame (UB);
                                outside the parity domain, frame left untouched                      */
     NFCS_ST_BAD_DESC = 15,  /* descriptor reaches past arena_bytes: frame not touched                */
-    NFCS_ST_FLAG_OVERLAP = 0x40 /* OR-ed in: IPv4 IHL < 5 with TCP/UDP/ICMP, so the L4 region
+    NFCS_ST_FLAG_OVERLAP = 0x40, /* OR-ed in: IPv4 IHL < 5 with TCP/UDP/ICMP, so the L4 region
                                    overlaps the IPv4 header; handled by the exact sequential path */
+    NFCS_ST_FLAG_FWD = 0x80     /* OR-ed in by nfcs_l3_forward_device: TTL decremented, MACs
+                                   rewritten, then the update_checksums() status in the low bits */
 };
 
 /* ---- error codes -------------------------------------------------------------------- */
@@ -136,6 +142,28 @@ NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_by
                               const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
                               uint32_t flags);
 
+/* ---- fused L3 forward ------------------------------------------------- */
+
+/* One next hop: the MACs Switch::process_received_packet writes (switch.hpp:286-289). */
+typedef struct nfcs_nexthop {
+    uint8_t dst_mac[6]; /* ARP-resolved next-hop MAC (arp_processor_.lookup_mac)      */
+    uint8_t src_mac[6]; /* egress interface MAC (interface_manager_.get_interface_mac) */
+} nfcs_nexthop;
+#define NFCS_NH_NONE 0xFFFFFFFFu
+
+/* Batched data path of the switch's transit-IPv4 forward (switch.hpp:247-294) in one HBM pass:
+ * for packet i with L3 EtherType IPv4 and an IPv4 header, TTL <= 1 -> NFCS_ST_TTL_EXPIRED;
+ * d_nh[i] >= table_n -> NFCS_ST_NO_ROUTE; else TTL--, dst/src MAC = d_table[d_nh[i]], then
+ * Packet::update_checksums(), status = its status | NFCS_ST_FLAG_FWD. Frames that are not
+ * forwarded are untouched. The control-plane steps (ACL, classification, is_my_ip, route and
+ * ARP lookup) stay with the caller and arrive as next-hop indexes.
+ *   d_nh     n device-resident u32 next-hop indexes (NFCS_NH_NONE = no route)
+ *   d_table  table_n device-resident next hops */
+NFCS_API int nfcs_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                                    const nfcs_desc* d_desc, const uint32_t* d_nh, uint32_t n,
+                                    const nfcs_nexthop* d_table, uint32_t table_n,
+                                    uint8_t* d_status, void* stream);
+
 /* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
 
 /* Lay out n frames of a config (packet indices first_index .. first_index+n-1), frame starts
@@ -173,6 +201,12 @@ NFCS_API int nfcs_stream_sync(nfcs_ctx* ctx, void* stream);
 NFCS_API int nfcs_time_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms);
+/* Same for nfcs_l3_forward_device (after the first launch every TTL has been decremented
+ * again, so repeated launches keep forwarding until TTLs reach 1: the bench restores them). */
+NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                                         const nfcs_desc* d_desc, const uint32_t* d_nh,
+                                         uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
+                                         uint8_t* d_status, int iters, void* stream, float* ms);
 
 #ifdef __cplusplus
 }

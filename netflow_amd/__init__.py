@@ -28,6 +28,9 @@ PATCH_DTYPE = np.dtype([("ip_off", "<u2"), ("l4_off", "<u2"), ("ip", "u1", (2,))
 ST_NONE, ST_V4, ST_V4_TCP, ST_V4_UDP, ST_V4_ICMP, ST_V4_L4SKIP = 0, 1, 2, 3, 4, 5
 ST_V6, ST_V6_TCP, ST_V6_UDP, ST_V6_L4SKIP, ST_OOB, ST_BAD_DESC = 6, 7, 8, 9, 14, 15
 ST_FLAG_OVERLAP = 0x40
+ST_NO_ROUTE, ST_NOT_IPV4, ST_TTL_EXPIRED, ST_FLAG_FWD = 11, 12, 13, 0x80
+NH_NONE = 0xFFFFFFFF
+NEXTHOP_DTYPE = np.dtype([("dst_mac", "u1", (6,)), ("src_mac", "u1", (6,))])
 CFG_C0, CFG_C1, CFG_C2, CFG_C3 = 0, 1, 2, 3
 HOST_PATCH_ONLY = 1
 PATCH_NONE = 0xFFFF
@@ -79,6 +82,11 @@ def _declare(L):
         "nfcs_stream_sync": ([_vp, _vp], ctypes.c_int),
         "nfcs_time_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, ctypes.c_int, _vp,
                                      ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "nfcs_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp, _vp],
+                                   ctypes.c_int),
+        "nfcs_time_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp,
+                                         ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_float)],
+                                        ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -202,6 +210,25 @@ class Engine:
                                       status.ctypes.data if want_status and n else None,
                                       HOST_PATCH_ONLY if patch_only else 0), "nfcs_update_host")
         return status
+
+    def l3_forward_device(self, arena, arena_bytes: int, desc, nh, n: int, table, table_n: int,
+                          status=None, stream=None):
+        """Fused transit-IPv4 forward (TTL--, MAC rewrite, update_checksums) on device frames;
+        nh = n u32 next-hop indexes, table = table_n nfcs_nexthop records (12 bytes each)."""
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_l3_forward_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), ptr(nh), n,
+                                            ptr(table), table_n, ptr(status), stream),
+               "nfcs_l3_forward_device")
+
+    def time_l3_forward_device(self, arena, arena_bytes, desc, nh, n, table, table_n, iters,
+                               status=None, stream=None) -> float:
+        ms = ctypes.c_float()
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_time_l3_forward_device(self.ctx, ptr(arena), arena_bytes, ptr(desc),
+                                                 ptr(nh), n, ptr(table), table_n, ptr(status),
+                                                 iters, stream, ctypes.byref(ms)),
+               "time_l3_forward_device")
+        return float(ms.value)
 
     def time_update_device(self, arena, arena_bytes, desc, n, iters, status=None, stream=None) -> float:
         ms = ctypes.c_float()

@@ -36,12 +36,9 @@ struct nfcs_ctx {
     int grid = 0;
     nfcs_patch* ws = nullptr;  // split-mode patch workspace (grown on demand)
     size_t ws_cap = 0;         // records
-    uint32_t* queue = nullptr; // kQueueSlots x kQueueWords work-queue counters
-    uint32_t qslot = 0;
     nfcs::Work work(size_t) {
         nfcs::Work w;
         w.patch = ws;
-        w.queue = queue + (size_t)(qslot++ % (nfcs::kQueueSlots - kSlots)) * nfcs::kQueueWords;
         return w;
     }
 };
@@ -62,11 +59,10 @@ hipError_t ensure_ws(nfcs_ctx* c, size_t n, uint64_t arena_bytes) {
     return e;
 }
 
-// host pipeline slot s: its own patch buffer as split workspace, its own queue slot
+// host pipeline slot s: its own patch buffer as split workspace
 nfcs::Work host_work(nfcs_ctx* c, int s) {
     nfcs::Work w;
     w.patch = c->d_patch[s];
-    w.queue = c->queue + (size_t)(nfcs::kQueueSlots - 1 - s) * nfcs::kQueueWords;
     return w;
 }
 
@@ -157,9 +153,6 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     c->grid = env_int("NFCS_GRID", 0);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_digest, sizeof(uint64_t));
-    const size_t qbytes = sizeof(uint32_t) * nfcs::kQueueWords * nfcs::kQueueSlots;
-    if (e == hipSuccess) e = hipMalloc(&c->queue, qbytes);
-    if (e == hipSuccess) e = hipMemset(c->queue, 0, qbytes);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
@@ -188,7 +181,6 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     }
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);
-    if (c->queue) (void)hipFree(c->queue);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -207,6 +199,19 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
     NFCS_HIP(ensure_ws(c, n, arena_bytes));
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
                                  pick(c, stream), c->variant, c->grid, c->work(n)));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                    const nfcs_desc* d_desc, const uint32_t* d_nh, uint32_t n,
+                                    const nfcs_nexthop* d_table, uint32_t table_n,
+                                    uint8_t* d_status, void* stream) {
+    if (!c) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!d_arena || !d_desc || !d_nh || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
+    if (table_n > 0 && (!d_table || ((uintptr_t)d_table & 3u))) return NFCS_EINVAL;
+    NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
+                                     d_status, pick(c, stream), c->grid));
     return NFCS_OK;
 }
 
@@ -400,6 +405,22 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,
                                      st, c->variant, c->grid, c->work(n)));
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                         const nfcs_desc* d_desc, const uint32_t* d_nh,
+                                         uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
+                                         uint8_t* d_status, int iters, void* stream, float* ms) {
+    if (!c || !ms || iters <= 0 || !d_arena || !d_desc || !d_nh) return NFCS_EINVAL;
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it)
+        NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
+                                         table_n, d_status, st, c->grid));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

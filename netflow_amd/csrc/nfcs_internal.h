@@ -30,10 +30,7 @@ struct DevInfo {
 // Per-context device workspace handed to the checksum launch.
 struct Work {
     nfcs_patch* patch = nullptr;  // split mode: patch records of the checksum pass
-    uint32_t* queue = nullptr;    // work-queue counters (kQueueWords, zero; kernels re-zero them)
 };
-constexpr int kQueueWords = 9 * 32;  // 8 per-XCD counters + a finish counter, 128 B apart
-constexpr int kQueueSlots = 16;      // rotating, so launches on different streams do not share
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
@@ -52,6 +49,11 @@ inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
 inline bool variant_needs_ws(int variant, uint64_t arena_bytes, uint32_t n) {
     return use_split(variant, arena_bytes, n);
 }
+
+hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
+                             const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
+                             const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
+                             hipStream_t stream, int grid);
 
 hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint64_t first,
                              uint32_t n, uint8_t* arena, uint64_t arena_bytes,

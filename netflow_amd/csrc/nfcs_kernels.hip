@@ -520,11 +520,21 @@ struct RowStage {
     uint32_t len;   // 0 unless live
     uint32_t p;
     uint32_t valid, bad;
+    uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
+    uint32_t mac[3];  // ... and its 12 MAC bytes
 };
 
-template <int K, int NT, int R = 16>
+// Fused L3 forward inputs (unused by the plain update).
+struct FwdArgs {
+    const uint32_t* nh;
+    const nfcs_nexthop* table;
+    uint32_t table_n;
+};
+
+template <int K, int NT, int R = 16, bool FWD = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl) {
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0,
+                   const FwdArgs* fa = nullptr) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     const bool bad = valid && ((d.off16 < base16) ||
@@ -537,6 +547,14 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     S.frame = arena + (live ? off : 0);
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
+    if (FWD) {  // the row's next-hop MACs, issued first so they land before the header slot
+        S.nh = nh;
+        const uint32_t* m = (nh < fa->table_n) ? (const uint32_t*)(fa->table + nh)
+                                               : (const uint32_t*)&g_zero16;
+        S.mac[0] = m[0];
+        S.mac[1] = m[1];
+        S.mac[2] = m[2];
+    }
     // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -550,26 +568,55 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
 // (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
-template <int K, int NT, int DBG = 0, int R = 16>
+template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
-                     nfcs_patch* patch) {
+                     nfcs_patch* patch, uint32_t table_n = 0) {
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
     if (DBG & 4) __builtin_amdgcn_s_setprio(3);  // finish the compute phase first
+    const bool live = S.valid && !S.bad;
+    uint4 h0 = S.v[0];
+    // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
+    // rewrite applied to the header registers, so the checksums below see the new header.
+    bool fwd = false, tagged = false;
+    uint32_t fst = NFCS_ST_NONE, ttl = 0;
+    if (FWD) {
+        const RowHdr<R> h{h0, rowbase4};
+        const uint32_t e12 = h.be16(12);
+        tagged = e12 == 0x8100u;  // ethernet() l2 = 18 (packet.hpp:410)
+        const uint32_t l3t = len < 14 ? 0u : (tagged ? (len >= 18 ? h.be16(16) : e12) : e12);
+        const bool v4 = l3t == 0x0800u && (tagged ? 38u : 34u) <= len;  // ipv4() present
+        ttl = tagged ? h.b(26) : h.b(22);
+        fst = !v4 ? (uint32_t)NFCS_ST_NOT_IPV4
+                  : (ttl <= 1 ? (uint32_t)NFCS_ST_TTL_EXPIRED
+                              : (S.nh >= table_n ? (uint32_t)NFCS_ST_NO_ROUTE : 0u));
+        fwd = live && fst == 0;
+        if (fwd && rl == 0) {  // dst_mac, src_mac (286-289)
+            h0.x = S.mac[0];
+            h0.y = S.mac[1];
+            h0.z = S.mac[2];
+        }
+        if (fwd && rl == 1) {  // ttl-- (279): byte 22 (dword 1) or 26 (dword 2), never borrows
+            if (tagged) h0.z -= 1u << 16;
+            else h0.y -= 1u << 16;
+        }
+    }
     RPlan P;
     if (DBG & 2) {
         P = rplan_none(NFCS_ST_V4_UDP);
         P.flags = F_IP | F_L4 | F_UDP; P.ipw = 24; P.rs = 34; P.re = len; P.fs = 40; P.corr = 0;
     } else {
-        P = fast_plan<R>(S.v[0], rowbase4, len);
+        P = fast_plan<R>(h0, rowbase4, len);
     }
-    const bool live = S.valid && !S.bad;
+    const bool act = live && (!FWD || fwd);  // rows whose checksums are updated
     // uncommon headers (IP options, IHL < 5, IHL past the frame) take the cold path below,
     // after the chunk registers are dead, so it adds nothing to the kernel's register peak
-    const bool slow = live && (P.st >> 8) != 0;
-    if (!live || slow) P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
-    uint32_t st = P.st;
+    const bool slow = act && (P.st >> 8) != 0;
+    if (!act || slow)
+        P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC
+                             : (FWD && live && !fwd) ? fst : (uint32_t)NFCS_ST_NONE);
+    uint32_t st = P.st | ((FWD && fwd) ? (uint32_t)NFCS_ST_FLAG_FWD : 0u);
     uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
     uint32_t l4w = NFCS_PATCH_NONE;
     // region sums (rows without an L4 region add nothing). rlv is opaque so the per-slot
@@ -619,6 +666,10 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             }
         }
     };
+    if (FWD && fwd && !(DBG & 1)) {  // the rewritten header bytes, before the cold path reads them
+        if (rl == 0) ((uint4*)frame)[0] = h0;  // frame len >= 34: chunk 0 is the frame's own
+        if (rl == 1) frame[tagged ? 26 : 22] = (uint8_t)(ttl - 1u);
+    }
     emit(S.valid && !slow, st, ipw, l4w, true);
     if (DBG & 4) __builtin_amdgcn_s_setprio(0);
     if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
@@ -626,6 +677,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
         // exact sequential emulation, which writes its own bytes) and the region is re-summed
         // from memory.
+        if (FWD) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // see the header stores
         RPlan Q = rplan_none(0);
         SeqOut o = {0, 0, 0, 0, 0};
         if (slow && rl == 0) {
@@ -659,19 +711,21 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             ipw2 = oip;
             l4w2 = ol4;
         }
+        if (FWD) st2 |= NFCS_ST_FLAG_FWD;
         emit(slow, st2, ipw2, l4w2, !seq);
     }
 }
 
 // Grid-stride over packets (the default grid has one workgroup per 4*64/R packets, so no
 // loop), 64/R packet rows per wave.
-template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1>
+template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false>
 __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
                                                                   uint64_t arena_bytes,
                                                                   const nfcs_desc* __restrict__ desc,
                                                                   uint32_t n, uint32_t base16,
                                                                   uint8_t* __restrict__ status,
-                                                                  nfcs_patch* __restrict__ patch) {
+                                                                  nfcs_patch* __restrict__ patch,
+                                                                  FwdArgs fa) {
     constexpr uint32_t PW = 64 / R;  // packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
@@ -683,83 +737,19 @@ __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __res
         const DescW<PW> D = Dn;
         if (pw + stride < n) Dn = load_descw<PW>(desc, pw + stride, n);  // prefetch (lgkmcnt)
         RowStage<K> S;
-        if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
-        row_stage<K, NT, R>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl);
-        if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-        row_process<K, NT, DBG, R>(S, rl, rowbase4, status, patch);
-    }
-}
-
-// Work-queue form: a resident grid of waves, each taking four-packet units from per-XCD
-// atomic counters (workgroups are dispatched round-robin over the 8 XCDs, so blockIdx & 7 is
-// the XCD and every XCD streams its own contiguous eighth of the batch; a drained XCD steals
-// from the next). The next unit's counter value and descriptors are fetched while the current
-// unit's frames are in flight, so a wave goes from one packet's compute straight into the next
-// packet's loads: no wave launch and no descriptor round trip between packets. The last wave
-// to finish re-zeroes the counters for the next launch.
-DEV uint32_t q_take(uint32_t* q, uint32_t x) {  // lane 0 takes a unit; result stays in a VGPR
-    uint32_t v = 0;
-    if ((threadIdx.x & 63u) == 0)
-        v = __hip_atomic_fetch_add(q + 32u * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-}
-
-template <int K, int NT, int R = 16, int DBG = 0>
-__global__ __launch_bounds__(kBlock) void update_queue_kernel(uint8_t* __restrict__ arena,
-                                                              uint64_t arena_bytes,
-                                                              const nfcs_desc* __restrict__ desc,
-                                                              uint32_t n, uint32_t base16,
-                                                              uint8_t* __restrict__ status,
-                                                              nfcs_patch* __restrict__ patch,
-                                                              uint32_t* __restrict__ q) {
-    constexpr uint32_t PW = 64 / R;  // packets per wave (one unit)
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
-    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint32_t units = (n + PW - 1) / PW;
-    const uint32_t per = (units + 7u) >> 3;
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
-    auto cnt = [&](uint32_t x) -> uint32_t {
-        const uint32_t lo = x * per;
-        return lo >= units ? 0u : min(per, units - lo);
-    };
-    uint32_t x = blockIdx.x & 7u, tries = 0;
-    // blocking take (first unit, and steals once an XCD's range is drained)
-    auto take_next = [&](uint32_t l) -> uint32_t {
-        for (;;) {
-            if (l < cnt(x)) return x * per + l;
-            x = (x + 1u) & 7u;
-            if (++tries >= 8u) return kNone;
-            l = rfl(q_take(q, x));
-        }
-    };
-    uint32_t cur = take_next(rfl(q_take(q, x)));
-    if (cur != kNone) {
-        DescW<PW> D = load_descw<PW>(desc, (uint64_t)cur * PW, n);
-        uint32_t pend = q_take(q, x);
-        for (;;) {
-            const uint64_t pw = (uint64_t)cur * PW;
-            RowStage<K> S;
-            row_stage<K, NT, R>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl);
-            const uint32_t nxt = take_next(rfl(pend));  // counted wait: the frames stay in flight
-            DescW<PW> Dn = D;
-            if (nxt != kNone) {
-                Dn = load_descw<PW>(desc, (uint64_t)nxt * PW, n);
-                pend = q_take(q, x);
-            }
-            row_process<K, NT, DBG, R>(S, rl, rowbase4, status, patch);
-            if (nxt == kNone) break;
-            cur = nxt;
-            D = Dn;
-        }
-    }
-    if (lane == 0) {
-        const uint32_t done = __hip_atomic_fetch_add(q + 32u * 8u, 1u, __ATOMIC_ACQ_REL,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (done == gridDim.x * (kBlock / kWave) - 1u) {
+        uint32_t nh = 0;
+        if (FWD) {  // the wave's PW next-hop indexes, scalar like the descriptors
+            uint32_t q[PW];
 #pragma unroll
-            for (uint32_t i = 0; i <= 8u; ++i)
-                __hip_atomic_store(q + 32u * i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? fa.nh[pw + i] : NFCS_NH_NONE;
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) nh |= (row == i) ? q[i] : 0u;
         }
+        if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
+        row_stage<K, NT, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
+                                 rl, nh, &fa);
+        if (DBG & 8) __builtin_amdgcn_s_setprio(0);
+        row_process<K, NT, DBG, R, FWD>(S, rl, rowbase4, status, patch, fa.table_n);
     }
 }
 
@@ -802,17 +792,12 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         const uint32_t need = (n + per_block - 1) / per_block;
         return grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
     };
+    const FwdArgs nofwd = {nullptr, nullptr, 0};
 #define NFCS_ROWSO(K, NT, R, DBG, OCC, PP)                                                       \
     hipLaunchKernelGGL((update_rows_kernel<K, NT, R, DBG, OCC>), dim3(rows_grid(R)), dim3(kBlock), \
-                       0, stream, arena, arena_bytes, desc, n, base16, status, PP)
+                       0, stream, arena, arena_bytes, desc, n, base16, status, PP, nofwd)
 #define NFCS_ROWSP(K, NT, R, DBG, PP) NFCS_ROWSO(K, NT, R, DBG, 1, PP)
 #define NFCS_ROWS(K, NT, R) NFCS_ROWSP(K, NT, R, 0, patch)
-    // work-queue form: a resident grid (5 waves per SIMD at this kernel's register count)
-    const int gq = grid > 0 ? grid : di.cus * 5;
-#define NFCS_QUEUE(K, NT, R, DBG)                                                                \
-    hipLaunchKernelGGL((update_queue_kernel<K, NT, R, DBG>), dim3(gq), dim3(kBlock), 0, stream,  \
-                       arena, arena_bytes, desc, n, base16, status, patch, work.queue)
-    if (use_split(variant, arena_bytes, n)) variant = 8;
     switch (variant) {
     default:
     case 0: NFCS_ROWS(6, 2, 16); break;   // 16-lane rows; header slot cached, payload evict-first
@@ -820,8 +805,6 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
     case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
     case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
-    case 6: NFCS_QUEUE(6, 2, 16, 0); break;   // work queue, 16-lane rows
-    case 7: NFCS_QUEUE(12, 2, 8, 0); break;   // work queue, 8-lane rows
     case 8: {  // split: checksum pass without frame stores, then the patch pass
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
@@ -841,8 +824,6 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 131: NFCS_ROWSO(6, 2, 16, 0, 6, patch); break;  // >= 6 waves per SIMD
     case 141: NFCS_ROWSP(6, 2, 16, 4, patch); break;  // high priority compute phase
     case 142: NFCS_ROWSP(6, 2, 16, 8, patch); break;  // high priority load issue
-    case 151: NFCS_QUEUE(6, 2, 16, 1); break;  // work queue, no frame stores
-    case 152: NFCS_QUEUE(6, 2, 16, 4); break;  // work queue, high priority compute phase
     case 155: NFCS_ROWS(12, 1, 8); break;      // 8-lane rows, all loads evict-first
     case 156: NFCS_ROWS(8, 2, 8); break;       // 8-lane rows, 8 slots
 #endif
@@ -850,7 +831,20 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 #undef NFCS_ROWS
 #undef NFCS_ROWSP
 #undef NFCS_ROWSO
-#undef NFCS_QUEUE
+    return hipGetLastError();
+}
+
+hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
+                             const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
+                             const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
+                             hipStream_t stream, int grid) {
+    (void)di;
+    if (n == 0) return hipSuccess;
+    const uint32_t need = (n + 15u) / 16u;
+    const int g = grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
+    const FwdArgs fa = {nh, table, table_n};
+    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, true>), dim3(g), dim3(kBlock), 0, stream,
+                       arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa);
     return hipGetLastError();
 }
 

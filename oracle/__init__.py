@@ -79,6 +79,11 @@ def lib() -> ctypes.CDLL:
         L.nfo_config_digest.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_int, _u64p, _u64p, _u64p]
         L.nfo_config_digest.restype = None
+        L.nfo_l3_forward.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        L.nfo_l3_forward.restype = ctypes.c_int
+        L.nfo_l3_forward_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, _u32p,
+                                           ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p]
+        L.nfo_l3_forward_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -100,6 +105,11 @@ def ref() -> ctypes.CDLL:
         R.nfref_update_batch.restype = None
         R.nfref_struct_sizes.argtypes = [ctypes.c_int]
         R.nfref_struct_sizes.restype = ctypes.c_int
+        R.nfref_l3_forward.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        R.nfref_l3_forward.restype = ctypes.c_int
+        R.nfref_l3_forward_batch.argtypes = [_u8p, ctypes.c_void_p, _u32p, ctypes.c_uint32, _u8p,
+                                             ctypes.c_uint32, ctypes.c_int]
+        R.nfref_l3_forward_batch.restype = None
         _ref = R
     return _ref
 
@@ -118,6 +128,34 @@ def ref_update_frame(frame: bytes) -> bytes:
     buf = np.frombuffer(bytearray(frame) + bytearray(64), dtype=np.uint8).copy()
     ref().nfref_update(_ptr(buf), len(frame))
     return bytes(buf[: len(frame)])
+
+
+def l3_forward_frame(frame: bytes, nh: bytes | None) -> tuple[bytes, int]:
+    """Oracle L3 forward of one frame (nh = 12 bytes {dst, src} or None); (bytes, status)."""
+    buf = np.frombuffer(bytearray(frame) + bytearray(16), dtype=np.uint8).copy()
+    h = None if nh is None else np.frombuffer(bytes(nh), dtype=np.uint8).copy()
+    st = lib().nfo_l3_forward(_ptr(buf), len(frame), None if h is None else _ptr(h))
+    return bytes(buf[: len(frame)]), st
+
+
+def ref_l3_forward_frame(frame: bytes, nh: bytes | None) -> tuple[bytes, int]:
+    """Reference L3 forward of one frame; (bytes, 1 if forwarded else 0)."""
+    buf = np.frombuffer(bytearray(frame) + bytearray(64), dtype=np.uint8).copy()
+    h = None if nh is None else np.frombuffer(bytes(nh), dtype=np.uint8).copy()
+    fw = ref().nfref_l3_forward(_ptr(buf), len(frame), None if h is None else _ptr(h))
+    return bytes(buf[: len(frame)]), fw
+
+
+def l3_forward_batch(arena: np.ndarray, desc: np.ndarray, nh_index: np.ndarray,
+                     table: np.ndarray) -> np.ndarray:
+    n = len(desc)
+    status = np.zeros(n, dtype=np.uint8)
+    nh_index = np.ascontiguousarray(nh_index, dtype=np.uint32)
+    table = np.ascontiguousarray(table, dtype=np.uint8).reshape(-1)
+    lib().nfo_l3_forward_batch(_ptr(arena), arena.nbytes, desc.ctypes.data, _ptr(nh_index, _u32p),
+                               n, _ptr(table) if table.size else None, table.size // 12,
+                               _ptr(status))
+    return status
 
 
 def update_batch(arena: np.ndarray, desc: np.ndarray, nthreads: int = 1,

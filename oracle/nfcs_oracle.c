@@ -151,6 +151,43 @@ int nfo_update(uint8_t* f, size_t len) {
     return (v4 ? NFO_ST_V4 : NFO_ST_V6) | ov;
 }
 
+/* Switch::process_received_packet, transit IPv4 (switch.hpp:247-294), restricted to the data
+ * path: the control-plane steps (ACL, classification, is_my_ip, route + ARP lookup) are the
+ * caller's and arrive as nh (NULL = no route / ARP miss). */
+int nfo_l3_forward(uint8_t* f, size_t len, const uint8_t* nh) {
+    if (len < 14) return NFO_ST_NOT_IPV4;            /* 248: ethernet() null -> L3 type 0 */
+    unsigned l3t = be16(f, 12);                      /* 257 */
+    size_t l2 = 14;
+    if (l3t == 0x8100) {                             /* 259-262: one tag; vlan() null keeps 0x8100 */
+        l2 = 18;                                     /* ethernet() set l2_header_size_ (packet.hpp:410) */
+        if (len >= 18) l3t = be16(f, 16);
+    }
+    if (l3t != 0x0800) return NFO_ST_NOT_IPV4;       /* 265 */
+    if (l2 + 20 > len) return NFO_ST_NOT_IPV4;       /* 266-267: ipv4() (packet.hpp:432-451) null */
+    if (f[l2 + 8] <= 1) return NFO_ST_TTL_EXPIRED;   /* 278: ICMP time exceeded, drop */
+    if (!nh) return NFO_ST_NO_ROUTE;                 /* 282-294: no route / ARP miss, drop */
+    f[l2 + 8]--;                                     /* 279 */
+    memcpy(f, nh, 12);                               /* 287-289: dst_mac, src_mac */
+    return nfo_update(f, len) | NFO_ST_FLAG_FWD;     /* 290 */
+}
+
+int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
+                         const uint32_t* nh_index, uint32_t n, const uint8_t* table,
+                         uint32_t table_n, uint8_t* status) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t off = (uint64_t)desc[i].off16 * 16;
+        int st;
+        if (off + (((uint64_t)desc[i].len + 15) & ~15ull) > arena_bytes) {
+            st = NFO_ST_BAD_DESC;
+        } else {
+            const uint8_t* nh = nh_index[i] < table_n ? table + (size_t)nh_index[i] * 12 : NULL;
+            st = nfo_l3_forward(arena + off, desc[i].len, nh);
+        }
+        if (status) status[i] = (uint8_t)st;
+    }
+    return 0;
+}
+
 /* result word as documented in nfcs.h: (ipv4 csum << 16) | l4 csum, 0 where not written */
 static uint32_t result_word(const uint8_t* f, size_t len, int st) {
     int base = st & 0x3F;

@@ -24,7 +24,8 @@ extern "C" {
 enum {
     NFO_ST_NONE = 0, NFO_ST_V4 = 1, NFO_ST_V4_TCP = 2, NFO_ST_V4_UDP = 3, NFO_ST_V4_ICMP = 4,
     NFO_ST_V4_L4SKIP = 5, NFO_ST_V6 = 6, NFO_ST_V6_TCP = 7, NFO_ST_V6_UDP = 8,
-    NFO_ST_V6_L4SKIP = 9, NFO_ST_OOB = 14, NFO_ST_BAD_DESC = 15, NFO_ST_FLAG_OVERLAP = 0x40
+    NFO_ST_V6_L4SKIP = 9, NFO_ST_NO_ROUTE = 11, NFO_ST_NOT_IPV4 = 12, NFO_ST_TTL_EXPIRED = 13,
+    NFO_ST_OOB = 14, NFO_ST_BAD_DESC = 15, NFO_ST_FLAG_OVERLAP = 0x40, NFO_ST_FLAG_FWD = 0x80
 };
 
 typedef struct nfo_desc { uint32_t off16; uint32_t len; } nfo_desc;
@@ -37,6 +38,18 @@ uint16_t nfo_calculate_checksum(const uint8_t* data, size_t len);
 /* batch over an arena; status may be NULL; returns 0 */
 int nfo_update_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc, uint32_t n,
                      uint8_t* status, uint32_t* result, int nthreads);
+
+/* Transit-IPv4 L3 forward of one frame as Switch::process_received_packet does it
+ * (switch.hpp:247-294): L3 EtherType after one tag, ipv4() present, TTL <= 1 -> dropped,
+ * TTL--, destination/source MAC rewrite, update_checksums(). nh = 12 bytes {dst[6], src[6]}
+ * of the resolved next hop, or NULL when the route / ARP lookup failed. Frames that are not
+ * forwarded are left untouched. Returns NFO_ST_NOT_IPV4 / TTL_EXPIRED / NO_ROUTE, or the
+ * update_checksums() status | NFO_ST_FLAG_FWD. */
+int nfo_l3_forward(uint8_t* frame, size_t len, const uint8_t* nh);
+/* batch: next hop of packet i = table[nh_index[i]] (12 bytes each), none if >= table_n */
+int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
+                         const uint32_t* nh_index, uint32_t n, const uint8_t* table,
+                         uint32_t table_n, uint8_t* status);
 
 /* synthetic configs (spec in DESIGN.md §6) */
 uint32_t nfo_config_len(int config, uint64_t seed, uint64_t index);

@@ -68,6 +68,57 @@ __attribute__((visibility("default"))) void nfref_update_batch(uint8_t* arena, c
     for (auto& t : th) t.join();
 }
 
+// The data-path part of Switch::process_received_packet for a transit IPv4 packet
+// (switch.hpp:247-294), driven through the reference's own Packet accessors: ethernet(),
+// vlan(), ipv4(), the TTL check/decrement, the MAC rewrite and update_checksums(). The
+// control-plane lookups are replaced by nh (12 bytes {dst, src}, or NULL for no route / ARP
+// miss). Returns 1 if forwarded, 0 if the switch would have dropped or diverted the packet
+// (untouched, as the caller sees it here).
+__attribute__((visibility("default"))) int nfref_l3_forward(uint8_t* frame, size_t len,
+                                                            const uint8_t* nh) {
+    Window w;
+    w.point(frame, len);
+    netflow::Packet pkt(&w.pb);
+    netflow::EthernetHeader* eth_hdr = pkt.ethernet();
+    uint16_t l2_type = eth_hdr ? ntohs(eth_hdr->ethertype) : 0;
+    uint16_t l3_type = l2_type;
+    if (l2_type == netflow::ETHERTYPE_VLAN) {
+        netflow::VlanHeader* vlan_hdr = pkt.vlan();
+        if (vlan_hdr) l3_type = ntohs(vlan_hdr->ethertype);
+    }
+    if (l3_type != netflow::ETHERTYPE_IPV4) return 0;
+    netflow::IPv4Header* ip_hdr = pkt.ipv4();
+    if (!ip_hdr) return 0;
+    if (ip_hdr->ttl <= 1) return 0;
+    if (!nh) return 0;
+    ip_hdr->ttl--;
+    eth_hdr->dst_mac = netflow::MacAddress(nh);
+    eth_hdr->src_mac = netflow::MacAddress(nh + 6);
+    pkt.update_checksums();
+    return 1;
+}
+
+// Batch of the above over an arena (next hop i = table[nh[i]], none if >= table_n) on
+// `nthreads` std::threads: the CPU baseline of the fused forward.
+__attribute__((visibility("default"))) void nfref_l3_forward_batch(uint8_t* arena, const void* desc_v,
+                                                                   const uint32_t* nh, uint32_t n,
+                                                                   const uint8_t* table,
+                                                                   uint32_t table_n, int nthreads) {
+    const Desc* desc = static_cast<const Desc*>(desc_v);
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; ++i)
+            nfref_l3_forward(arena + (uint64_t)desc[i].off16 * 16, desc[i].len,
+                             nh[i] < table_n ? table + (size_t)nh[i] * 12 : nullptr);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t)
+        th.emplace_back(work, (uint32_t)((uint64_t)n * t / nthreads),
+                        (uint32_t)((uint64_t)n * (t + 1) / nthreads));
+    work(0, (uint32_t)((uint64_t)n / nthreads));
+    for (auto& t : th) t.join();
+}
+
 __attribute__((visibility("default"))) int nfref_struct_sizes(int which) {
     switch (which) {
     case 0: return (int)sizeof(netflow::EthernetHeader);

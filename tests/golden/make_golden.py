@@ -11,6 +11,9 @@ reference does on:
                     length, frame_hash before and after the reference's update_checksums()
   configs.json      digests of the synthetic configs C0..C3 before/after the
                     reference, at full BASELINE sizes, plus per-rank shards for multi-GPU
+  l3fwd_ref.npz     the fused L3 forward (switch.hpp:247-294 data path: TTL check/decrement,
+  kat_l3.json       MAC rewrite, update_checksums()) through the reference's Packet on fuzz
+                    frames with TTL overrides and next-hop indexes, and on the KAT frames
 The fixtures are data only: frames in, frames/hashes out.
 """
 from __future__ import annotations
@@ -120,6 +123,102 @@ def make_fuzz(R):
     print("fuzz_ref.npz:", FUZZ_N, "frames; statuses", np.unique(st, return_counts=True))
 
 
+L3_SEED = 20250621
+L3_N = 32768
+
+
+def l3_table():
+    """8 next hops {dst[6], src[6]} (fixed bytes)."""
+    rng = np.random.default_rng(L3_SEED)
+    return rng.integers(0, 256, size=(8, 12), dtype=np.uint8)
+
+
+def l3_inputs(n=L3_N):
+    """Fuzz frames (seed L3_SEED) with a TTL override and a next-hop index per frame:
+    ttl_set[i] = 255 means no override, else the TTL byte at l2+8 is set to it (frames long
+    enough); nh_index = i % 9 (8 = no route)."""
+    frames = oracle.fuzz_frames(L3_SEED, 0, n)
+    ttl_set = np.full(n, 255, dtype=np.uint8)
+    ttl_set[0::5] = 1
+    ttl_set[1::7] = 0
+    ttl_set[2::11] = 2
+    out = []
+    for i, f in enumerate(frames):
+        b = bytearray(f)
+        l2 = 18 if len(b) >= 14 and b[12:14] == b"\x81\x00" else 14
+        if ttl_set[i] != 255 and len(b) > l2 + 8:
+            b[l2 + 8] = int(ttl_set[i])
+        out.append(bytes(b))
+    nh_index = (np.arange(n) % 9).astype(np.uint32)
+    return out, ttl_set, nh_index
+
+
+def make_l3(R):
+    """Fused L3 forward (switch.hpp:247-294 data path) through the reference's Packet."""
+    L = oracle.lib()
+    table = l3_table()
+    frames, ttl_set, nh_index = l3_inputs()
+    n = len(frames)
+    h_in = np.zeros(n, dtype=np.uint64)
+    h_out = np.zeros(n, dtype=np.uint64)
+    fwd = np.zeros(n, dtype=np.uint8)
+    st = np.zeros(n, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        nh = bytes(table[nh_index[i]]) if nh_index[i] < 8 else None
+        b = np.frombuffer(f + bytes(16), dtype=np.uint8).copy()
+        h_in[i] = L.nfo_frame_hash(oracle._ptr(b), len(f))
+        o_orc, s = oracle.l3_forward_frame(f, nh)
+        st[i] = s
+        if (s & 0x3F) == 14:  # outside the reference's defined domain (IHL past the frame)
+            continue
+        o, fw = oracle.ref_l3_forward_frame(f, nh)
+        assert o == o_orc and fw == (1 if s & 0x80 else 0), i
+        fwd[i] = fw
+        ob = np.frombuffer(o + bytes(16), dtype=np.uint8).copy()
+        h_out[i] = L.nfo_frame_hash(oracle._ptr(ob), len(f))
+    np.savez_compressed(os.path.join(OUT, "l3fwd_ref.npz"), seed=np.uint64(L3_SEED),
+                        lens=np.array([len(f) for f in frames], dtype=np.uint16), ttl_set=ttl_set,
+                        nh_index=nh_index, table=table, hash_in=h_in, hash_out=h_out,
+                        forwarded=fwd, oracle_status=st)
+    print("l3fwd_ref.npz:", n, "frames; statuses", np.unique(st, return_counts=True))
+    # known answers: the KAT frames forwarded through next hop 0, plus drop cases
+    kats = {}
+    for name, fr in kat_frames().items():
+        for tag, nh in (("fwd", bytes(table[0])), ("noroute", None)):
+            o, fw = oracle.ref_l3_forward_frame(fr, nh)
+            o2, s = oracle.l3_forward_frame(fr, nh)
+            assert o == o2
+            kats[f"{name}/{tag}"] = {"in": fr.hex(), "nh": None if nh is None else nh.hex(),
+                                     "out": o.hex(), "forwarded": fw, "status": s}
+    ttl1 = bytearray(kat_frames()["B_packet_test_udp"])
+    ttl1[22] = 1
+    o, fw = oracle.ref_l3_forward_frame(bytes(ttl1), bytes(table[1]))
+    kats["B_packet_test_udp/ttl1"] = {"in": bytes(ttl1).hex(), "nh": bytes(table[1]).hex(),
+                                      "out": o.hex(), "forwarded": fw,
+                                      "status": oracle.l3_forward_frame(bytes(ttl1), bytes(table[1]))[1]}
+    with open(os.path.join(OUT, "kat_l3.json"), "w") as fh:
+        json.dump(kats, fh, indent=1, sort_keys=True)
+    print("kat_l3.json:", len(kats), "cases")
+    # bench workload: C1, one fused forward, next hop i % 9 of l3_table() (8 = no route)
+    res = json.load(open(os.path.join(OUT, "configs.json")))
+    n = 1 << 20
+    M = (1 << 64) - 1
+    dout = 0
+    tab = np.ascontiguousarray(table.reshape(-1))
+    for lo in range(0, n, CHUNK):
+        m = min(CHUNK, n - lo)
+        arena, desc = oracle.gen_config(1, CONFIG_SEED, lo, m)
+        nh = ((np.arange(lo, lo + m)) % 9).astype(np.uint32)
+        R.nfref_l3_forward_batch(oracle._ptr(arena), desc.ctypes.data, oracle._ptr(nh, oracle._u32p),
+                                 m, oracle._ptr(tab), 8, 8)
+        dout = (dout + oracle.digest(arena, desc, lo)) & M
+    res["l3fwd_c1"] = {"first": 0, "n": n, "nh": "i % 9 (8 = no route), table = l3_table()",
+                       "table": table.tobytes().hex(), "digest_out": f"{dout:016x}"}
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+    print(f"l3fwd C1 digest {dout:016x}")
+
+
 def ref_config_digest(R, config, seed, first, n, nthreads=8):
     """Digest of config packets [first, first+n) before and after the REFERENCE."""
     din = dout = 0
@@ -161,10 +260,12 @@ def make_configs(R):
 if __name__ == "__main__":
     oracle.build(ref=True)
     R = oracle.ref()
-    what = sys.argv[1:] or ["kat", "fuzz", "configs"]
+    what = sys.argv[1:] or ["kat", "fuzz", "configs", "l3"]
     if "kat" in what:
         make_kat(R)
     if "fuzz" in what:
         make_fuzz(R)
     if "configs" in what:
         make_configs(R)
+    if "l3" in what:
+        make_l3(R)
