@@ -9,10 +9,12 @@ so per-GPU work is fixed (weak scaling) and there is no collective on the data p
 only meet at the timing barriers.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1] [--packets n] [--no-cpu]
-                  [--op update|l3fwd]
+                  [--op update|l3fwd|flowkey]
 
 --op l3fwd measures the fused transit-IPv4 forward instead (TTL--, MAC rewrite,
 update_checksums; nfcs_l3_forward_device) on C1 with next hop i % 9 (8 = no route).
+--op flowkey measures PacketClassifier::extract_flow_key + hash_flow (SURVEY.md §8 f4;
+nfcs_flow_keys_device: 64-byte records + u32 hashes) in packets/s.
 
 Prints ONE JSON line on rank 0. `value` = sum over ranks of frame bytes per step / the max
 over ranks of the timed wall time per step. `roofline` uses the kernel's HIP-event time on its
@@ -143,7 +145,21 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
     n = {0: 1024, 1: 1 << 20, 2: 1 << 17, 3: 1 << 21}[config]
     arena, desc = oracle.gen_config(config, SEED, 0, n)
     nbytes = float(desc["len"].astype(np.float64).sum())
-    if op == "l3fwd":
+    recs = hashes = None
+    if op == "flowkey":
+        recs = np.zeros((n, 64), dtype=np.uint8)
+        hashes = np.zeros(n, dtype=np.uint32)
+        if kind == "reference":
+            R = oracle.ref()
+            run = lambda: R.nfref_flow_keys_batch(oracle._ptr(arena), desc.ctypes.data, n,
+                                                  oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p),
+                                                  threads)
+        else:
+            L = oracle.lib()
+            run = lambda: L.nfo_flow_keys_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
+                                                oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p))
+            threads = 1
+    elif op == "l3fwd":
         g = golden_l3()
         table = np.frombuffer(bytes.fromhex(g["table"]), dtype=np.uint8).copy()
         nh = (np.arange(n) % 9).astype(np.uint32)
@@ -165,15 +181,23 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
         L = oracle.lib()
         run = lambda: L.nfo_update_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
                                          None, None, threads)
+    # l3fwd mutates TTLs (each pass forwards once): restore the frames before every pass,
+    # outside the timed part
+    pristine = arena.copy() if op == "l3fwd" else None
     run()  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
+    reps, el = 0, 0.0
+    while el < min_seconds:
+        if pristine is not None:
+            np.copyto(arena, pristine)
+        t0 = time.perf_counter()
         run()
+        el += time.perf_counter() - t0
         reps += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            break
     gbs = nbytes * reps / el / 1e9
+    if op == "flowkey":
+        return {"value": round(n * reps / el / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
+                "kind": kind, "sample": f"{n} packets of config C{config} x {reps} passes, "
+                                        f"{threads} threads, g++ -O2, {el:.1f} s"}
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
             "sample": f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes, "
                       f"{threads} threads, g++ -O2, {el:.1f} s"}
@@ -205,7 +229,7 @@ def main():
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--op", choices=["update", "l3fwd"], default="update")
+    ap.add_argument("--op", choices=["update", "l3fwd", "flowkey"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -232,6 +256,15 @@ def main():
         step = lambda: eng.l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8)
         regen = lambda: (eng.gen_config_device(args.config, SEED, first, n, d_arena, nbytes, d_desc),
                          eng.sync())
+    elif args.op == "flowkey":
+        d_keys = eng.alloc(64 * n)
+        d_hash = eng.alloc(4 * n)
+        # moved per packet: the header line (min(len, 128) bytes) + 8 B descriptor read,
+        # 64 B record + 4 B hash written
+        hdr = float(np.minimum(hdesc["len"].astype(np.float64), 128.0).sum())
+        algo_bytes = hdr + 76.0 * n
+        step = lambda: eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
+        regen = lambda: None
     else:
         step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
         regen = lambda: None
@@ -273,6 +306,10 @@ def main():
         step()
         eng.sync()
         want = g3["digest_out"] if (args.config == 1 and first == 0 and n == g3["n"]) else None
+    elif args.op == "flowkey":
+        ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
+                                          args.steps) / args.steps
+        want = None  # parity of the flow keys: tests/test_flow_keys.py (reference fixtures)
     else:
         ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
         # parity of what was measured: digest of the updated arena vs the reference's
@@ -282,12 +319,16 @@ def main():
     parity_ok = None if want is None else (got == want)
     parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    traffic = None if l3 else load_traffic(args.config, n)
+    traffic = load_traffic(args.config, n) if args.op == "update" else None
+    fk = args.op == "flowkey"
+    total_packets = D.sum(float(n))
     out = {
-        "metric": "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X"
-                  + (" (fused L3 forward: TTL--, MAC rewrite, checksums)" if l3 else ""),
-        "value": round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
-        "unit": "GB/s",
+        "metric": ("flow keys + hash_flow per second, batched packets, MI355X" if fk else
+                   "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X"
+                   + (" (fused L3 forward: TTL--, MAC rewrite, checksums)" if l3 else "")),
+        "value": round(total_packets / (wall / args.steps) / 1e6, 2) if fk else
+                 round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
+        "unit": "Mpkt/s" if fk else "GB/s",
         "n_gpus": ws,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -297,7 +338,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
-        "config": {"workload": WORKLOAD[args.config] + (", fused L3 forward (next hop i % 9)" if l3 else ""),
+        "config": {"workload": WORKLOAD[args.config] + (", fused L3 forward (next hop i % 9)" if l3 else "")
+                   + (", flow keys (header line only)" if fk else ""),
                    "packets_per_gpu": n, "frame_align": args.align,
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -164,6 +164,34 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t ar
                                     const nfcs_nexthop* d_table, uint32_t table_n,
                                     uint8_t* d_status, void* stream);
 
+/* ---- flow-key extract + hash -------------------------------------------- */
+
+/* PacketClassifier::FlowKey + hash_flow (packet_classifier.hpp:15-56, packet_classifier.cpp:12-108)
+ * as one 64-byte record per packet. Integers little-endian in host order (the reference stores
+ * ntohs/ntohl values); an IPv4 address is the host-order u32 key.src_ip/dst_ip in bytes 0-3 of
+ * its 16-byte field (the rest zero), an IPv6 address its 16 bytes. */
+typedef struct nfcs_flow_key {
+    uint32_t hash;        /* PacketClassifier::hash_flow(key)                          */
+    uint16_t vlan_id;     /* key.vlan_id (TCI & 0xFFF of the first tag, 0 if none)      */
+    uint16_t ethertype;   /* key.ethertype (inner EtherType after one tag)             */
+    uint8_t src_mac[6];
+    uint8_t dst_mac[6];
+    uint8_t protocol;     /* IPv4 protocol / IPv6 next header                          */
+    uint8_t is_ipv6;
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t reserved[6];  /* zero */
+    uint8_t src_ip[16];
+    uint8_t dst_ip[16];
+} nfcs_flow_key;
+
+/* Batched PacketClassifier::extract_flow_key + hash_flow over device-resident frames (read
+ * only: the first 128 bytes of each frame at most). d_keys (n records) and d_hash (n u32) are
+ * each optional; a descriptor outside the arena yields a zero record and hash 0. */
+NFCS_API int nfcs_flow_keys_device(nfcs_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                                   const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
+                                   uint32_t* d_hash, void* stream);
+
 /* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
 
 /* Lay out n frames of a config (packet indices first_index .. first_index+n-1), frame starts
@@ -201,6 +229,10 @@ NFCS_API int nfcs_stream_sync(nfcs_ctx* ctx, void* stream);
 NFCS_API int nfcs_time_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms);
+/* Same for nfcs_flow_keys_device. */
+NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                                        const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
+                                        uint32_t* d_hash, int iters, void* stream, float* ms);
 /* Same for nfcs_l3_forward_device (after the first launch every TTL has been decremented
  * again, so repeated launches keep forwarding until TTLs reach 1: the bench restores them). */
 NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,

@@ -31,6 +31,11 @@ ST_FLAG_OVERLAP = 0x40
 ST_NO_ROUTE, ST_NOT_IPV4, ST_TTL_EXPIRED, ST_FLAG_FWD = 11, 12, 13, 0x80
 NH_NONE = 0xFFFFFFFF
 NEXTHOP_DTYPE = np.dtype([("dst_mac", "u1", (6,)), ("src_mac", "u1", (6,))])
+FLOW_KEY_DTYPE = np.dtype([("hash", "<u4"), ("vlan_id", "<u2"), ("ethertype", "<u2"),
+                           ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)), ("protocol", "u1"),
+                           ("is_ipv6", "u1"), ("src_port", "<u2"), ("dst_port", "<u2"),
+                           ("reserved", "u1", (6,)), ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,))])
+assert FLOW_KEY_DTYPE.itemsize == 64
 CFG_C0, CFG_C1, CFG_C2, CFG_C3 = 0, 1, 2, 3
 HOST_PATCH_ONLY = 1
 PATCH_NONE = 0xFFFF
@@ -84,6 +89,9 @@ def _declare(L):
                                      ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp, _vp],
                                    ctypes.c_int),
+        "nfcs_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
+        "nfcs_time_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, ctypes.c_int, _vp,
+                                        ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_time_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp,
                                          ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_float)],
                                         ctypes.c_int),
@@ -219,6 +227,23 @@ class Engine:
         _check(lib().nfcs_l3_forward_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), ptr(nh), n,
                                             ptr(table), table_n, ptr(status), stream),
                "nfcs_l3_forward_device")
+
+    def flow_keys_device(self, arena, arena_bytes: int, desc, n: int, keys=None, hashes=None,
+                         stream=None):
+        """PacketClassifier::extract_flow_key + hash_flow on device frames: n 64-byte
+        FLOW_KEY_DTYPE records and/or n u32 hashes."""
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_flow_keys_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n, ptr(keys),
+                                           ptr(hashes), stream), "nfcs_flow_keys_device")
+
+    def time_flow_keys_device(self, arena, arena_bytes, desc, n, keys, hashes, iters,
+                              stream=None) -> float:
+        ms = ctypes.c_float()
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_time_flow_keys_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n,
+                                                ptr(keys), ptr(hashes), iters, stream,
+                                                ctypes.byref(ms)), "time_flow_keys_device")
+        return float(ms.value)
 
     def time_l3_forward_device(self, arena, arena_bytes, desc, nh, n, table, table_n, iters,
                                status=None, stream=None) -> float:

@@ -215,6 +215,18 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
     return NFCS_OK;
 }
 
+NFCS_API int nfcs_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
+                                   const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
+                                   uint32_t* d_hash, void* stream) {
+    if (!c) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u) || ((uintptr_t)d_keys & 15u))
+        return NFCS_EINVAL;
+    NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash,
+                                    pick(c, stream)));
+    return NFCS_OK;
+}
+
 NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
                               const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
                               uint32_t flags) {
@@ -421,6 +433,20 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
                                          table_n, d_status, st, c->grid));
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
+                                        const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
+                                        uint32_t* d_hash, int iters, void* stream, float* ms) {
+    if (!c || !ms || iters <= 0 || !d_arena || !d_desc) return NFCS_EINVAL;
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it)
+        NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

@@ -627,7 +627,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     asm volatile("" : "+v"(rlv));
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc_slot(acc, S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
+    for (int k = 0; k < K; ++k) acc_slot(acc, k == 0 ? h0 : S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
     // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t nre = (re + 15u) >> 4;
     const uint32_t cmax = wave_max_rows<R>(nre);
@@ -845,6 +845,110 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     const FwdArgs fa = {nh, table, table_n};
     hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, true>), dim3(g), dim3(kBlock), 0, stream,
                        arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa);
+    return hipGetLastError();
+}
+
+// ---- flow-key extract + hash -----------------------------------------------
+// PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) on the first
+// 128 bytes of each frame: one 8-lane DPP row per packet (lane rl holds frame bytes
+// 16rl..16rl+15, one global_load_dwordx4), 8 packets per wave. Every field the key reads lies
+// below byte 82 (l2 18 + IHL 60 + 4 port bytes), so one slot covers it. Fields reach the row by
+// the same RowHdr broadcasts and 802.1Q view as the checksum plan; the record's 16 dwords are
+// stored by lanes 0-3 (64 contiguous bytes per packet, 512 per wave).
+static_assert(sizeof(nfcs_flow_key) == 64, "nfcs_flow_key is a 64-byte record");
+
+DEV uint32_t be32x(uint32_t le) { return __builtin_bswap32(le); }
+
+__global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __restrict__ arena,
+                                                           uint64_t arena_bytes,
+                                                           const nfcs_desc* __restrict__ desc,
+                                                           uint32_t n, nfcs_flow_key* __restrict__ keys,
+                                                           uint32_t* __restrict__ hashes) {
+    constexpr int R = 8;
+    constexpr uint32_t PW = 64 / R;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    if (pw >= n) return;
+    const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
+    const uint64_t p = pw + row;
+    const uint64_t off = (uint64_t)d.off16 * 16u;
+    const bool live = p < n && off + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes;
+    const uint32_t len = live ? d.len : 0u;
+    const uint4* src = (const uint4*)(arena + (live ? off : 0));
+    const uint4 c0 = ld16<0>((rl * 16u < len) ? src + rl : &g_zero16);
+
+    const RowHdr<R> h{c0, rowbase4};
+    const bool eth = len >= 14;
+    const uint32_t dw0 = h.dw(0), dw1 = h.dw(1), dw2 = h.dw(2);
+    const uint32_t e12 = h.be16(12);
+    const bool tagged = e12 == 0x8100u;
+    uint32_t et = eth ? e12 : 0u, vlan = 0;
+    if (eth && tagged && len >= 18) {  // has_vlan / vlan_id / vlan() (packet.hpp:603-618)
+        vlan = h.be16(14) & 0x0FFFu;
+        et = h.be16(16);
+    }
+    const uint32_t sh = tagged ? 4u : 0u;  // l2 = 18 after a tag (ethernet(), packet.hpp:410)
+    const RowHdr<R> V{strip_tag(c0, tagged), rowbase4};  // view byte o = frame byte o + sh
+    const bool v4 = et == 0x0800u, v6 = et == 0x86DDu;
+    uint32_t proto = 0, sp = 0, dp = 0, s4 = 0, d4 = 0;
+    uint32_t s6[4] = {0, 0, 0, 0}, d6[4] = {0, 0, 0, 0};
+    uint32_t l4 = 0;  // view offset
+    bool hdr = false;
+    if (v4 && 34u + sh <= len) {  // ipv4() present
+        s4 = be32x(V.dw(7) >> 16 | V.dw(8) << 16);   // view bytes 26..29
+        d4 = be32x(V.dw(8) >> 16 | V.dw(9) << 16);   // view bytes 30..33
+        proto = V.b(23);
+        l4 = 14u + (V.b(14) & 15u) * 4u;
+        hdr = true;
+    } else if (v6 && 54u + sh <= len) {  // ipv6() present
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {  // view bytes 22..37 and 38..53, as LE dwords
+            s6[j] = V.dw(5 + j) >> 16 | V.dw(6 + j) << 16;
+            d6[j] = V.dw(9 + j) >> 16 | V.dw(10 + j) << 16;
+        }
+        proto = V.b(20);
+        l4 = 54u;
+        hdr = true;
+    }
+    // tcp() needs l4 + 19 <= len (19-byte TcpHeader), udp() l4 + 8 (packet.hpp:473-535)
+    if (hdr && ((proto == 6 && l4 + sh + 19u <= len) || (proto == 17 && l4 + sh + 8u <= len))) {
+        sp = V.be16(l4);        // runtime offset: ds_bpermute
+        dp = V.be16(l4 + 2u);
+    }
+    const uint32_t m0 = eth ? dw0 : 0u, m1 = eth ? dw1 : 0u, m2 = eth ? dw2 : 0u;
+    // hash_flow (82-108): byte i of each MAC / IPv6 address at shift (i % 4) * 8
+    uint32_t hv = m0 ^ (m1 & 0xFFFFu) ^ ((m1 >> 16) | (m2 << 16)) ^ (m2 >> 16);
+    hv ^= vlan ^ (et << 16);
+    if (v6) hv ^= s6[0] ^ s6[1] ^ s6[2] ^ s6[3] ^ d6[0] ^ d6[1] ^ d6[2] ^ d6[3];
+    else hv ^= s4 ^ d4;
+    hv ^= proto ^ (sp << 16) ^ dp;
+    if (!live) hv = 0;
+    if (keys && rl < 4) {
+        uint4 r;
+        if (rl == 0) {
+            r = make_uint4(hv, vlan | (et << 16), (m1 >> 16) | (m2 << 16), (m2 >> 16) | (m0 << 16));
+        } else if (rl == 1) {
+            r = make_uint4((m0 >> 16) | (m1 << 16), proto | ((v6 ? 1u : 0u) << 8) | (sp << 16), dp, 0u);
+        } else if (rl == 2) {
+            r = v6 ? make_uint4(s6[0], s6[1], s6[2], s6[3]) : make_uint4(s4, 0u, 0u, 0u);
+        } else {
+            r = v6 ? make_uint4(d6[0], d6[1], d6[2], d6[3]) : make_uint4(d4, 0u, 0u, 0u);
+        }
+        if (!live) r = make_uint4(0u, 0u, 0u, 0u);
+        if (p < n) ((uint4*)(keys + p))[rl] = r;
+    }
+    if (hashes && rl == 0 && p < n) hashes[p] = hv;
+}
+
+hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
+                            const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,
+                            uint32_t* hashes, hipStream_t stream) {
+    (void)di;
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 31u) / 32u;  // 8 rows per wave, 4 waves per workgroup
+    hipLaunchKernelGGL(flow_keys_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, arena_bytes,
+                       desc, n, keys, hashes);
     return hipGetLastError();
 }
 

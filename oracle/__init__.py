@@ -84,6 +84,11 @@ def lib() -> ctypes.CDLL:
         L.nfo_l3_forward_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, _u32p,
                                            ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p]
         L.nfo_l3_forward_batch.restype = ctypes.c_int
+        L.nfo_flow_key.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        L.nfo_flow_key.restype = ctypes.c_uint32
+        L.nfo_flow_keys_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                          _u8p, _u32p]
+        L.nfo_flow_keys_batch.restype = None
         _lib = L
     return _lib
 
@@ -110,6 +115,11 @@ def ref() -> ctypes.CDLL:
         R.nfref_l3_forward_batch.argtypes = [_u8p, ctypes.c_void_p, _u32p, ctypes.c_uint32, _u8p,
                                              ctypes.c_uint32, ctypes.c_int]
         R.nfref_l3_forward_batch.restype = None
+        R.nfref_flow_key.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        R.nfref_flow_key.restype = ctypes.c_uint32
+        R.nfref_flow_keys_batch.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint32, _u8p, _u32p,
+                                            ctypes.c_int]
+        R.nfref_flow_keys_batch.restype = None
         _ref = R
     return _ref
 
@@ -156,6 +166,31 @@ def l3_forward_batch(arena: np.ndarray, desc: np.ndarray, nh_index: np.ndarray,
                                n, _ptr(table) if table.size else None, table.size // 12,
                                _ptr(status))
     return status
+
+
+def flow_key(frame: bytes) -> tuple[bytes, int]:
+    """Oracle extract_flow_key + hash_flow of one frame: (64-byte record, hash)."""
+    buf = np.frombuffer(bytes(frame) + bytes(16), dtype=np.uint8).copy()
+    rec = np.zeros(64, dtype=np.uint8)
+    h = lib().nfo_flow_key(_ptr(buf), len(frame), _ptr(rec))
+    return bytes(rec), int(h)
+
+
+def ref_flow_key(frame: bytes) -> tuple[bytes, int]:
+    """Reference PacketClassifier::extract_flow_key + hash_flow: (64-byte record, hash)."""
+    buf = np.frombuffer(bytes(frame) + bytes(64), dtype=np.uint8).copy()
+    rec = np.zeros(64, dtype=np.uint8)
+    h = ref().nfref_flow_key(_ptr(buf), len(frame), _ptr(rec))
+    return bytes(rec), int(h)
+
+
+def flow_keys_batch(arena: np.ndarray, desc: np.ndarray):
+    n = len(desc)
+    recs = np.zeros((n, 64), dtype=np.uint8)
+    hashes = np.zeros(n, dtype=np.uint32)
+    lib().nfo_flow_keys_batch(_ptr(arena), arena.nbytes, desc.ctypes.data, n, _ptr(recs),
+                              _ptr(hashes, _u32p))
+    return recs, hashes
 
 
 def update_batch(arena: np.ndarray, desc: np.ndarray, nthreads: int = 1,

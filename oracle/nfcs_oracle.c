@@ -188,6 +188,120 @@ int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* d
     return 0;
 }
 
+/* ---- flow key ----------------------------------------------------------- */
+static inline void put16le(uint8_t* p, unsigned v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+static inline void put32le(uint8_t* p, uint32_t v) {
+    for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+static inline uint32_t be32(const uint8_t* f, size_t o) {
+    return ((uint32_t)f[o] << 24) | ((uint32_t)f[o + 1] << 16) | ((uint32_t)f[o + 2] << 8) | f[o + 3];
+}
+static inline uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* extract_flow_key (packet_classifier.cpp:12-80) with the Packet accessors it calls:
+ * ethernet()/src_mac()/dst_mac() need len >= 14; has_vlan()/vlan_id()/vlan() need the tag and
+ * len >= 18 (get_header<VlanHeader>(14)); ipv4()/ipv6() need the effective EtherType and
+ * l2 + 20 / l2 + 40 <= len (packet.hpp:432-470); tcp()/udp() need the IPv4 protocol / IPv6
+ * next header and l4 + 19 (the 19-byte TcpHeader) / l4 + 8 <= len, l4 = l2 + IHL*4 or l2 + 40
+ * (packet.hpp:473-535). hash_flow (82-108) XORs byte i of each MAC / IPv6 address at shift
+ * (i % 4) * 8, i.e. the little-endian dwords. */
+uint32_t nfo_flow_key(const uint8_t* f, size_t len, uint8_t* rec) {
+    uint8_t src_mac[6] = {0}, dst_mac[6] = {0}, src6[16] = {0}, dst6[16] = {0};
+    unsigned vlan = 0, et = 0, proto = 0, sp = 0, dp = 0;
+    int is6 = 0;
+    uint32_t sip = 0, dip = 0;
+    size_t l2 = 14;
+    if (len >= 14) {
+        memcpy(dst_mac, f, 6);
+        memcpy(src_mac, f + 6, 6);
+        et = be16(f, 12);
+        if (et == 0x8100) {
+            l2 = 18;
+            if (len >= 18) {
+                vlan = be16(f, 14) & 0x0FFF;
+                et = be16(f, 16);
+            }
+        }
+    }
+    if (et == 0x0800) {
+        if (l2 + 20 <= len) {
+            sip = be32(f, l2 + 12);
+            dip = be32(f, l2 + 16);
+            proto = f[l2 + 9];
+            const size_t l4 = l2 + (size_t)(f[l2] & 15) * 4;
+            if (proto == 6 && l4 + 19 <= len) { sp = be16(f, l4); dp = be16(f, l4 + 2); }
+            if (proto == 17 && l4 + 8 <= len) { sp = be16(f, l4); dp = be16(f, l4 + 2); }
+        }
+    } else if (et == 0x86DD) {
+        is6 = 1;
+        if (l2 + 40 <= len) {
+            memcpy(src6, f + l2 + 8, 16);
+            memcpy(dst6, f + l2 + 24, 16);
+            proto = f[l2 + 6];
+            const size_t l4 = l2 + 40;
+            if (proto == 6 && l4 + 19 <= len) { sp = be16(f, l4); dp = be16(f, l4 + 2); }
+            if (proto == 17 && l4 + 8 <= len) { sp = be16(f, l4); dp = be16(f, l4 + 2); }
+        }
+    }
+    uint32_t h = 0;
+    for (int i = 0; i < 6; ++i) {
+        h ^= (uint32_t)src_mac[i] << (i % 4 * 8);
+        h ^= (uint32_t)dst_mac[i] << (i % 4 * 8);
+    }
+    h ^= vlan;
+    h ^= (uint32_t)et << 16;
+    if (is6) {
+        for (int i = 0; i < 16; ++i) {
+            h ^= (uint32_t)src6[i] << ((i % 4) * 8);
+            h ^= (uint32_t)dst6[i] << ((i % 4) * 8);
+        }
+    } else {
+        h ^= sip;
+        h ^= dip;
+    }
+    h ^= proto;
+    h ^= (uint32_t)sp << 16;
+    h ^= dp;
+    if (rec) {
+        memset(rec, 0, 64);
+        put32le(rec, h);
+        put16le(rec + 4, vlan);
+        put16le(rec + 6, et);
+        memcpy(rec + 8, src_mac, 6);
+        memcpy(rec + 14, dst_mac, 6);
+        rec[20] = (uint8_t)proto;
+        rec[21] = (uint8_t)is6;
+        put16le(rec + 22, sp);
+        put16le(rec + 24, dp);
+        if (is6) {
+            memcpy(rec + 32, src6, 16);
+            memcpy(rec + 48, dst6, 16);
+        } else {
+            put32le(rec + 32, sip);
+            put32le(rec + 48, dip);
+        }
+    }
+    (void)le32;
+    return h;
+}
+
+void nfo_flow_keys_batch(const uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
+                         uint32_t n, uint8_t* recs, uint32_t* hashes) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t off = (uint64_t)desc[i].off16 * 16;
+        uint8_t* r = recs ? recs + (size_t)i * 64 : NULL;
+        uint32_t h = 0;
+        if (off + (((uint64_t)desc[i].len + 15) & ~15ull) <= arena_bytes) {
+            h = nfo_flow_key(arena + off, desc[i].len, r);
+        } else if (r) {
+            memset(r, 0, 64);
+        }
+        if (hashes) hashes[i] = h;
+    }
+}
+
 /* result word as documented in nfcs.h: (ipv4 csum << 16) | l4 csum, 0 where not written */
 static uint32_t result_word(const uint8_t* f, size_t len, int st) {
     int base = st & 0x3F;

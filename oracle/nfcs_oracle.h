@@ -51,6 +51,12 @@ int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* d
                          const uint32_t* nh_index, uint32_t n, const uint8_t* table,
                          uint32_t table_n, uint8_t* status);
 
+/* PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) of one frame,
+ * written as the 64-byte nfcs_flow_key record of include/nfcs.h; returns the hash. */
+uint32_t nfo_flow_key(const uint8_t* frame, size_t len, uint8_t* rec /* 64 bytes */);
+void nfo_flow_keys_batch(const uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
+                         uint32_t n, uint8_t* recs /* n x 64, may be NULL */, uint32_t* hashes);
+
 /* synthetic configs (spec in DESIGN.md §6) */
 uint32_t nfo_config_len(int config, uint64_t seed, uint64_t index);
 void nfo_config_frame(int config, uint64_t seed, uint64_t index, uint8_t* out /* >= len */);

@@ -10,8 +10,10 @@
 // (packet_buffer.hpp:10-111) whose data window is pointed at the caller's frame, so the
 // reference mutates the caller's bytes in place exactly as it would its own buffer.
 #include <netflow++/packet.hpp>
+#include <netflow++/packet_classifier.hpp>
 
 #include <cstdint>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -110,6 +112,62 @@ __attribute__((visibility("default"))) void nfref_l3_forward_batch(uint8_t* aren
         for (uint32_t i = lo; i < hi; ++i)
             nfref_l3_forward(arena + (uint64_t)desc[i].off16 * 16, desc[i].len,
                              nh[i] < table_n ? table + (size_t)nh[i] * 12 : nullptr);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t)
+        th.emplace_back(work, (uint32_t)((uint64_t)n * t / nthreads),
+                        (uint32_t)((uint64_t)n * (t + 1) / nthreads));
+    work(0, (uint32_t)((uint64_t)n / nthreads));
+    for (auto& t : th) t.join();
+}
+
+// PacketClassifier::extract_flow_key + hash_flow (src/netflow++/packet_classifier.cpp:12-108,
+// compiled from the reference source by oracle/Makefile), serialised into the 64-byte record
+// of include/nfcs.h (nfcs_flow_key). Returns the hash.
+static void put16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+static void put32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+
+__attribute__((visibility("default"))) uint32_t nfref_flow_key(uint8_t* frame, size_t len,
+                                                               uint8_t* rec /* 64 bytes */) {
+    Window w;
+    w.point(frame, len);
+    netflow::Packet pkt(&w.pb);
+    netflow::PacketClassifier pc;
+    const netflow::PacketClassifier::FlowKey k = pc.extract_flow_key(pkt);
+    const uint32_t h = netflow::PacketClassifier::hash_flow(k);
+    std::memset(rec, 0, 64);
+    put32(rec + 0, h);
+    put16(rec + 4, k.vlan_id);
+    put16(rec + 6, k.ethertype);
+    std::memcpy(rec + 8, k.src_mac.bytes, 6);
+    std::memcpy(rec + 14, k.dst_mac.bytes, 6);
+    rec[20] = k.protocol;
+    rec[21] = k.is_ipv6 ? 1 : 0;
+    put16(rec + 22, k.src_port);
+    put16(rec + 24, k.dst_port);
+    if (k.is_ipv6) {
+        std::memcpy(rec + 32, k.src_ipv6.data(), 16);
+        std::memcpy(rec + 48, k.dst_ipv6.data(), 16);
+    } else {
+        put32(rec + 32, k.src_ip);
+        put32(rec + 48, k.dst_ip);
+    }
+    return h;
+}
+
+// Batch of the above on `nthreads` std::threads (records may be NULL): the CPU baseline.
+__attribute__((visibility("default"))) void nfref_flow_keys_batch(uint8_t* arena, const void* desc_v,
+                                                                  uint32_t n, uint8_t* recs,
+                                                                  uint32_t* hashes, int nthreads) {
+    const Desc* desc = static_cast<const Desc*>(desc_v);
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](uint32_t lo, uint32_t hi) {
+        uint8_t tmp[64];
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint32_t h = nfref_flow_key(arena + (uint64_t)desc[i].off16 * 16, desc[i].len,
+                                              recs ? recs + (size_t)i * 64 : tmp);
+            if (hashes) hashes[i] = h;
+        }
     };
     std::vector<std::thread> th;
     for (int t = 1; t < nthreads; ++t)

@@ -14,6 +14,9 @@ reference does on:
   l3fwd_ref.npz     the fused L3 forward (switch.hpp:247-294 data path: TTL check/decrement,
   kat_l3.json       MAC rewrite, update_checksums()) through the reference's Packet on fuzz
                     frames with TTL overrides and next-hop indexes, and on the KAT frames
+  kat_flow.json     PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp,
+  flow_ref.npz      compiled from the reference source) on builder-shaped frames and on fuzz
+                    frames: 64-byte records (nfcs_flow_key layout) and hashes
 The fixtures are data only: frames in, frames/hashes out.
 """
 from __future__ import annotations
@@ -219,6 +222,82 @@ def make_l3(R):
     print(f"l3fwd C1 digest {dout:016x}")
 
 
+FLOW_SEED = 20250622
+FLOW_N = 32768
+
+
+def flow_kat_frames():
+    """Frames shaped like the reference's packet_classifier_test.cpp builders (Ethernet / VLAN /
+    IPv4 / IPv6 / TCP / UDP helpers at :16-146, MACs and IPv6 addresses of its fixture :158-167)."""
+    sm, dm = bytes([0, 1, 2, 3, 4, 5]), bytes([0xAA, 0xBB, 0xCC, 0xDD, 0xEE, 0xFF])
+    s6 = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [1])
+    d6 = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [2])
+
+    def eth(et):
+        return dm + sm + be16(et)
+
+    def vlan(vid, prio, et):
+        return be16((prio << 13) | vid) + be16(et)
+
+    def ip4(src, dst, proto, tl=20):
+        return bytes([0x45, 0]) + be16(tl) + be16(12345) + bytes(2) + bytes([64, proto]) + bytes(2) + \
+            src.to_bytes(4, "big") + dst.to_bytes(4, "big")
+
+    def ip6(nh, plen=0):
+        return (6 << 28).to_bytes(4, "big") + be16(plen) + bytes([nh, 64]) + s6 + d6
+
+    def tcp(sp, dp):
+        return be16(sp) + be16(dp) + (1000).to_bytes(4, "big") + bytes(4) + bytes([0x50, 0]) + \
+            be16(8192) + bytes(4)
+
+    def udp(sp, dp):
+        return be16(sp) + be16(dp) + be16(8) + bytes(2)
+
+    k = {}
+    k["arp"] = eth(0x0806) + bytes(28)
+    k["ipv4_proto0"] = eth(0x0800) + ip4(0xC0A80101, 0xC0A80102, 0)
+    k["ipv6_nh0"] = eth(0x86DD) + ip6(0)
+    k["vlan101_ipv4_tcp"] = eth(0x8100) + vlan(101, 3, 0x0800) + ip4(0x0A000001, 0x0A000002, 6, 40) + tcp(12345, 80)
+    k["ipv4_tcp"] = eth(0x0800) + ip4(0xC0A80101, 0xC0A80102, 6, 40) + tcp(1024, 443)
+    k["ipv4_udp"] = eth(0x0800) + ip4(0xC0A80101, 0xC0A80102, 17, 28) + udp(5353, 53)
+    k["ipv6_tcp"] = eth(0x86DD) + ip6(6, 20) + tcp(40000, 22)
+    k["ipv6_udp"] = eth(0x86DD) + ip6(17, 8) + udp(546, 547)
+    k["vlan_ipv6_udp"] = eth(0x8100) + vlan(4095, 7, 0x86DD) + ip6(17, 8) + udp(1, 2)
+    k["ipv4_tcp_19B_edge"] = (eth(0x0800) + ip4(1, 2, 6, 39) + tcp(7, 9))[:14 + 20 + 19]
+    k["ipv4_tcp_18B_short"] = (eth(0x0800) + ip4(1, 2, 6, 38) + tcp(7, 9))[:14 + 20 + 18]
+    k["vlan_runt"] = eth(0x8100) + bytes(2)
+    k["runt_13"] = eth(0x0800)[:13]
+    k["ipv4_ihl7_udp"] = eth(0x0800) + bytes([0x47, 0]) + be16(36) + bytes(4) + bytes([64, 17]) + \
+        bytes(2) + bytes([1, 2, 3, 4, 5, 6, 7, 8]) + bytes(8) + udp(11, 22)
+    return k
+
+
+def make_flow(R):
+    """Flow key + hash (packet_classifier.cpp:12-108) through the reference's PacketClassifier."""
+    L = oracle.lib()
+    kats = {}
+    for name, fr in flow_kat_frames().items():
+        rec, h = oracle.ref_flow_key(fr)
+        assert (rec, h) == oracle.flow_key(fr), name
+        kats[name] = {"in": fr.hex(), "record": rec.hex(), "hash": h}
+    with open(os.path.join(OUT, "kat_flow.json"), "w") as fh:
+        json.dump(kats, fh, indent=1, sort_keys=True)
+    frames = oracle.fuzz_frames(FLOW_SEED, 0, FLOW_N)
+    hashes = np.zeros(FLOW_N, dtype=np.uint32)
+    rdig = np.zeros(FLOW_N, dtype=np.uint64)
+    for i, f in enumerate(frames):
+        rec, h = oracle.ref_flow_key(f)
+        assert (rec, h) == oracle.flow_key(f), i
+        hashes[i] = h
+        rb = np.frombuffer(rec + bytes(16), dtype=np.uint8).copy()
+        rdig[i] = L.nfo_frame_hash(oracle._ptr(rb), 64)
+    np.savez_compressed(os.path.join(OUT, "flow_ref.npz"), seed=np.uint64(FLOW_SEED),
+                        lens=np.array([len(f) for f in frames], dtype=np.uint16), hash=hashes,
+                        record_digest=rdig)
+    print("kat_flow.json:", len(kats), "frames; flow_ref.npz:", FLOW_N, "frames,",
+          len(np.unique(hashes)), "distinct hashes")
+
+
 def ref_config_digest(R, config, seed, first, n, nthreads=8):
     """Digest of config packets [first, first+n) before and after the REFERENCE."""
     din = dout = 0
@@ -260,7 +339,7 @@ def make_configs(R):
 if __name__ == "__main__":
     oracle.build(ref=True)
     R = oracle.ref()
-    what = sys.argv[1:] or ["kat", "fuzz", "configs", "l3"]
+    what = sys.argv[1:] or ["kat", "fuzz", "configs", "l3", "flow"]
     if "kat" in what:
         make_kat(R)
     if "fuzz" in what:
@@ -269,3 +348,5 @@ if __name__ == "__main__":
         make_configs(R)
     if "l3" in what:
         make_l3(R)
+    if "flow" in what:
+        make_flow(R)
