@@ -896,8 +896,8 @@ __global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __rest
     uint32_t l4 = 0;  // view offset
     bool hdr = false;
     if (v4 && 34u + sh <= len) {  // ipv4() present
-        s4 = be32x(V.dw(7) >> 16 | V.dw(8) << 16);   // view bytes 26..29
-        d4 = be32x(V.dw(8) >> 16 | V.dw(9) << 16);   // view bytes 30..33
+        s4 = be32x(V.dw(6) >> 16 | V.dw(7) << 16);   // view bytes 26..29
+        d4 = be32x(V.dw(7) >> 16 | V.dw(8) << 16);   // view bytes 30..33
         proto = V.b(23);
         l4 = 14u + (V.b(14) & 15u) * 4u;
         hdr = true;
