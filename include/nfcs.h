@@ -80,6 +80,10 @@ enum {
     NFCS_ST_OOB = 14,       /* IPv4 with l2 + IHL*4 > len: the reference reads past the frame (UB);
                                outside the parity domain, frame left untouched                      */
     NFCS_ST_BAD_DESC = 15,  /* descriptor reaches past arena_bytes: frame not touched                */
+    NFCS_ST_VLAN_FAIL = 16, /* nfcs_vlan_device: push_vlan / pop_vlan returned false (no tag to pop,
+                               runt frame, no tailroom): frame and length untouched                 */
+    NFCS_ST_FLAG_VLAN = 0x20, /* OR-ed in by nfcs_vlan_device: the tag was pushed / re-written /
+                                 popped, then the update_checksums() status in the low bits      */
     NFCS_ST_FLAG_OVERLAP = 0x40, /* OR-ed in: IPv4 IHL < 5 with TCP/UDP/ICMP, so the L4 region
                                    overlaps the IPv4 header; handled by the exact sequential path */
     NFCS_ST_FLAG_FWD = 0x80     /* OR-ed in by nfcs_l3_forward_device: TTL decremented, MACs
@@ -164,6 +168,40 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t ar
                                     const nfcs_nexthop* d_table, uint32_t table_n,
                                     uint8_t* d_status, void* stream);
 
+/* ---- VLAN push / pop + checksum ---------------------------------------- */
+
+/* One VLAN edit per packet as a u32: the operation in bits 30-31, the priority in bits 13-15
+ * and the VLAN id in bits 0-11 (the arguments of Packet::push_vlan, masked as
+ * VlanHeader::set_vlan_id / set_priority mask them, packet.hpp:185-190). */
+#define NFCS_VLAN_NOP 0x00000000u
+#define NFCS_VLAN_PUSH 0x40000000u /* Packet::push_vlan(vid, prio)  packet.hpp:655-692 */
+#define NFCS_VLAN_POP 0x80000000u  /* Packet::pop_vlan()            packet.hpp:694-720 */
+#define NFCS_VLAN_OP_MASK 0xC0000000u
+#define NFCS_VLAN_PUSH_OP(vid, prio) \
+    (NFCS_VLAN_PUSH | (((uint32_t)(prio) & 7u) << 13) | ((uint32_t)(vid) & 0xFFFu))
+
+/* Batched Packet::push_vlan / pop_vlan, each followed by the update_checksums() it ends with, on
+ * device-resident frames in one HBM pass (VlanManager::process_ingress / process_egress call
+ * them per packet, vlan_manager.cpp:90,159,174). Per packet i with edit op_i (d_ops[i], or
+ * op_all when d_ops is NULL) and buffer capacity cap_i (d_caps[i], or cap_all; the bytes the
+ * frame's buffer holds from the frame start, i.e. PacketBuffer capacity minus headroom):
+ *   push, frame already tagged   -> TCI id/priority rewritten in place (DEI kept), checksums
+ *   push, untagged, len+4 <= cap -> bytes [14, len) move up by 4, 0x8100 + TCI inserted at 12,
+ *                                   len += 4, checksums
+ *   pop, tagged and len >= 18    -> bytes [18, len) move down by 4, inner EtherType at 12,
+ *                                   len -= 4, checksums
+ *   anything else                -> untouched: NFCS_ST_VLAN_FAIL (the reference returns false)
+ *                                   or NFCS_ST_NONE (NFCS_VLAN_NOP).
+ * d_desc[i].len is updated in place. Frame bytes past the new length keep the values the
+ * reference's memmove leaves. A push needs the 16-byte chunks up to len + 4 inside the arena
+ * (else NFCS_ST_BAD_DESC) and cap_i must not reach into another frame.
+ *   d_status  optional (NULL) n status bytes: NFCS_ST_FLAG_VLAN | update_checksums() status,
+ *             NFCS_ST_VLAN_FAIL, NFCS_ST_NONE or NFCS_ST_BAD_DESC */
+NFCS_API int nfcs_vlan_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                              nfcs_desc* d_desc, uint32_t n, const uint32_t* d_ops,
+                              uint32_t op_all, const uint32_t* d_caps, uint32_t cap_all,
+                              uint8_t* d_status, void* stream);
+
 /* ---- flow-key extract + hash -------------------------------------------- */
 
 /* PacketClassifier::FlowKey + hash_flow (packet_classifier.hpp:15-56, packet_classifier.cpp:12-108)
@@ -239,6 +277,13 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64
                                          const nfcs_desc* d_desc, const uint32_t* d_nh,
                                          uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
                                          uint8_t* d_status, int iters, void* stream, float* ms);
+
+/* Same for nfcs_vlan_device with a uniform edit: launches alternate between op_all (even
+ * iterations) and op_alt (odd), so a push / pop pair leaves every frame as it was. */
+NFCS_API int nfcs_time_vlan_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                                   nfcs_desc* d_desc, uint32_t n, uint32_t op_all,
+                                   uint32_t op_alt, uint32_t cap_all, uint8_t* d_status, int iters,
+                                   void* stream, float* ms);
 
 #ifdef __cplusplus
 }

@@ -30,6 +30,14 @@ ST_V6, ST_V6_TCP, ST_V6_UDP, ST_V6_L4SKIP, ST_OOB, ST_BAD_DESC = 6, 7, 8, 9, 14,
 ST_FLAG_OVERLAP = 0x40
 ST_NO_ROUTE, ST_NOT_IPV4, ST_TTL_EXPIRED, ST_FLAG_FWD = 11, 12, 13, 0x80
 NH_NONE = 0xFFFFFFFF
+ST_VLAN_FAIL, ST_FLAG_VLAN = 16, 0x20
+VLAN_NOP, VLAN_PUSH, VLAN_POP = 0, 0x40000000, 0x80000000
+
+
+def vlan_push_op(vid: int, prio: int = 0) -> int:
+    """NFCS_VLAN_PUSH_OP(vid, prio): the edit word of Packet::push_vlan(vid, prio)."""
+    return VLAN_PUSH | ((prio & 7) << 13) | (vid & 0xFFF)
+
 NEXTHOP_DTYPE = np.dtype([("dst_mac", "u1", (6,)), ("src_mac", "u1", (6,))])
 FLOW_KEY_DTYPE = np.dtype([("hash", "<u4"), ("vlan_id", "<u2"), ("ethertype", "<u2"),
                            ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)), ("protocol", "u1"),
@@ -89,6 +97,10 @@ def _declare(L):
                                      ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp, _vp],
                                    ctypes.c_int),
+        "nfcs_vlan_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp],
+                             ctypes.c_int),
+        "nfcs_time_vlan_device": ([_vp, _vp, _u64, _vp, _u32, _u32, _u32, _u32, _vp, ctypes.c_int,
+                                   _vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_time_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, ctypes.c_int, _vp,
                                         ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
@@ -227,6 +239,25 @@ class Engine:
         _check(lib().nfcs_l3_forward_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), ptr(nh), n,
                                             ptr(table), table_n, ptr(status), stream),
                "nfcs_l3_forward_device")
+
+    def vlan_device(self, arena, arena_bytes: int, desc, n: int, ops=None, op_all: int = 0,
+                    caps=None, cap_all: int = 0, status=None, stream=None):
+        """Batched Packet::push_vlan / pop_vlan + update_checksums on device frames; desc
+        lengths are updated in place. ops: n u32 edit words (or op_all for every packet),
+        caps: n u32 buffer capacities from the frame start (or cap_all)."""
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_vlan_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n, ptr(ops),
+                                      op_all, ptr(caps), cap_all, ptr(status), stream),
+               "nfcs_vlan_device")
+
+    def time_vlan_device(self, arena, arena_bytes, desc, n, op_all, op_alt, cap_all, iters,
+                         status=None, stream=None) -> float:
+        ms = ctypes.c_float()
+        ptr = lambda b: None if b is None else (b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        _check(lib().nfcs_time_vlan_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n, op_all,
+                                           op_alt, cap_all, ptr(status), iters, stream,
+                                           ctypes.byref(ms)), "time_vlan_device")
+        return float(ms.value)
 
     def flow_keys_device(self, arena, arena_bytes: int, desc, n: int, keys=None, hashes=None,
                          stream=None):

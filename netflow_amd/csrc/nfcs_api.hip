@@ -215,6 +215,19 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
     return NFCS_OK;
 }
 
+NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                              nfcs_desc* d_desc, uint32_t n, const uint32_t* d_ops,
+                              uint32_t op_all, const uint32_t* d_caps, uint32_t cap_all,
+                              uint8_t* d_status, void* stream) {
+    if (!c) return NFCS_EINVAL;
+    if (n == 0) return NFCS_OK;
+    if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
+    if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
+    NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
+                               cap_all, d_status, pick(c, stream)));
+    return NFCS_OK;
+}
+
 NFCS_API int nfcs_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
                                    const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
                                    uint32_t* d_hash, void* stream) {
@@ -433,6 +446,22 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
                                          table_n, d_status, st, c->grid));
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                   nfcs_desc* d_desc, uint32_t n, uint32_t op_all,
+                                   uint32_t op_alt, uint32_t cap_all, uint8_t* d_status, int iters,
+                                   void* stream, float* ms) {
+    if (!c || !ms || iters <= 0 || !d_arena || !d_desc) return NFCS_EINVAL;
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it)
+        NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
+                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

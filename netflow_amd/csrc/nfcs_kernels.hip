@@ -848,6 +848,292 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     return hipGetLastError();
 }
 
+// ---- VLAN push / pop + checksum ----------------------------------------------
+// Packet::push_vlan(vid, prio) / pop_vlan() (packet.hpp:655-720) and the update_checksums() they
+// end with, in one pass per frame. One 16-lane row per packet as in update_rows_kernel: the row
+// loads the frame's chunks (K slots of 16 lanes), builds the EDITED frame's chunks in registers
+// (a 4-byte shift is one DPP row_shr:1 / row_shl:1 of a dword plus three register moves per
+// chunk; the chunk that crosses a slot boundary takes a row_newbcast from the neighbouring
+// slot), plans update_checksums() on the edited header, sums the edited chunks, patches the
+// checksum bytes into the chunk registers and stores the edited frame with 16-byte stores. So
+// the memmove, the tag and the checksums cost one read and one write of the frame.
+//   * frames longer than one batch (K*16 chunks) are processed batch by batch, in ascending
+//     order: a push carries the last dword of the previous batch's old chunks in a register
+//     (the store of batch b overwrites it), a pop loads the first dword of the next batch;
+//     batch 0 is then stored before the loop and the checksum bytes are stored at the end by
+//     the lanes that stored their chunks;
+//   * bytes of a frame's last chunk past the bytes the reference writes keep their old values
+//     (the slot's tail is rewritten with what it held), so the arena matches the reference's
+//     memmove byte for byte;
+//   * uncommon headers take the same cold path as update_rows_kernel, after the edited frame is
+//     in memory.
+enum : uint32_t { VM_NONE = 0, VM_FAIL = 1, VM_RETAG = 2, VM_PUSH = 3, VM_POP = 4 };
+
+// Chunk bytes at frame offsets >= wend keep their old values.
+DEV uint4 keep_tail(const uint4& nv, const uint4& ov, uint32_t o, uint32_t wend) {
+    uint32_t r[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const int nb = (int)wend - (int)(o + 4u * j);
+        const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+        r[j] = (comp(nv, j) & m) | (comp(ov, j) & ~m);
+    }
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+// Byte i (0..15) of a chunk register := b.
+DEV uint4 put_byte(const uint4& v, uint32_t i, uint32_t b) {
+    uint32_t r[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t sh = 8u * (i & 3u);
+        const uint32_t m = ((i >> 2) == j) ? (0xFFu << sh) : 0u;
+        r[j] = (comp(v, j) & ~m) | ((b << sh) & m);
+    }
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+DEV uint32_t dpp_prev(uint32_t x) {  // lane rl gets lane rl-1 of its row (0 for rl = 0)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xF, 0xF, true);
+}
+DEV uint32_t dpp_next(uint32_t x) {  // lane rl gets lane rl+1 of its row (0 for rl = 15)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xF, 0xF, true);
+}
+
+// Edited chunks of one batch. v: old chunks rl + 16k (+ cb); prevw: for a push, the old dword
+// just before this batch (the row's lane 15 of the previous batch); nextx: for a pop, the old
+// dword just after it. Batch 0 (first = true) builds the new bytes 12-15 in chunk 0.
+template <int K>
+DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t rl, bool first,
+                   uint32_t prevw, uint32_t nextx, uint32_t tag_dw, uint32_t cb, uint32_t wend) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint4 e = v[k];
+        if (mode == VM_PUSH) {  // new[o] = old[o - 4] for o >= 16
+            uint32_t pw = dpp_prev(v[k].w);
+            const uint32_t lw = (k > 0) ? row_bcast<15, 16>(v[k - 1].w) : prevw;
+            if (rl == 0) pw = lw;
+            e = make_uint4(pw, v[k].x, v[k].y, v[k].z);
+            if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, tag_dw);
+        } else if (mode == VM_POP) {  // new[o] = old[o + 4] for o >= 12
+            uint32_t nx = dpp_next(v[k].x);
+            const uint32_t fx = (k + 1 < K) ? row_bcast<0, 16>(v[k + 1 < K ? k + 1 : k].x) : nextx;
+            if (rl == 15) nx = fx;
+            e = make_uint4(v[k].y, v[k].z, v[k].w, nx);
+            if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, nx);
+        } else if (mode == VM_RETAG) {
+            if (first && k == 0 && rl == 0) e.w = tag_dw;
+        }
+        const uint32_t c = cb + rl + 16u * (uint32_t)k;
+        nv[k] = keep_tail(e, v[k], 16u * c, wend);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
+                                                           uint64_t arena_bytes,
+                                                           nfcs_desc* __restrict__ desc, uint32_t n,
+                                                           const uint32_t* __restrict__ ops,
+                                                           uint32_t op_all,
+                                                           const uint32_t* __restrict__ caps,
+                                                           uint32_t cap_all,
+                                                           uint8_t* __restrict__ status) {
+    constexpr int R = 16;
+    constexpr uint32_t PW = 4, KR = (uint32_t)(K * R);
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
+    const uint32_t rowbase4 = (lane & ~15u) * 4u;
+    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    if (pw >= n) return;
+    const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
+    uint32_t op = op_all, cap = cap_all;
+    {  // the wave's four edit words / capacities: scalar loads, like the descriptors
+        uint32_t q[PW], r[PW];
+#pragma unroll
+        for (uint32_t i = 0; i < PW; ++i) {
+            q[i] = (ops && pw + i < n) ? ops[pw + i] : op_all;
+            r[i] = (caps && pw + i < n) ? caps[pw + i] : cap_all;
+        }
+        if (ops) { op = 0; for (uint32_t i = 0; i < PW; ++i) op |= (row == i) ? q[i] : 0u; }
+        if (caps) { cap = 0; for (uint32_t i = 0; i < PW; ++i) cap |= (row == i) ? r[i] : 0u; }
+    }
+    const uint64_t p = pw + row;
+    const bool valid = p < n;
+    const uint32_t kind = op & NFCS_VLAN_OP_MASK;
+    const uint64_t off = (uint64_t)d.off16 * 16u;
+    const uint64_t need = (uint64_t)d.len + (kind == NFCS_VLAN_PUSH ? 4u : 0u);
+    const bool bad = valid && (off + ((need + 15u) & ~15ull) > arena_bytes);
+    const bool live = valid && !bad;
+    const uint32_t len = live ? d.len : 0u;
+    uint8_t* frame = arena + (live ? off : 0);
+    const uint4* src = (const uint4*)frame;
+    const uint32_t nl = live ? (uint32_t)((need + 15u) >> 4) : 0u;  // old chunks to load
+
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = rl + (uint32_t)R * k;
+        v[k] = ld16<0>((c < nl) ? src + c : &g_zero16);
+    }
+    // pop: the old dword after batch 0 (first dword of chunk KR)
+    const uint32_t nx0 = *(const uint32_t*)((KR < nl) ? src + KR : &g_zero16);
+
+    // the edit the reference makes (packet.hpp:655-720), decided on the old header
+    const RowHdr<R> h{v[0], rowbase4};
+    const bool tagged = len >= 14 && h.be16(12) == 0x8100u;  // has_vlan() (603-606)
+    uint32_t mode = VM_NONE;
+    if (live && kind == NFCS_VLAN_PUSH)
+        mode = len < 14 ? VM_FAIL : tagged ? VM_RETAG : (len + 4u > cap ? VM_FAIL : VM_PUSH);
+    else if (live && kind == NFCS_VLAN_POP)
+        mode = (!tagged || len < 18) ? VM_FAIL : VM_POP;
+    const bool act = mode >= VM_RETAG;
+    const uint32_t vid = op & 0x0FFFu, prio = (op >> 13) & 7u;
+    const uint32_t tci_old = h.be16(14);
+    const uint32_t tci = ((mode == VM_RETAG ? tci_old : 0u) & 0x1000u) | (prio << 13) | vid;  // 185-190
+    const uint32_t tag_dw = (mode == VM_RETAG) ? ((comp(v[0], 3) & 0xFFFFu) | (bswap16(tci) << 16))
+                                               : (0x81u | (bswap16(tci) << 16));
+    const uint32_t nlen = mode == VM_PUSH ? len + 4u : mode == VM_POP ? len - 4u : len;
+    // bytes the reference writes end at wend: the moved frame, or bytes 14-15 of the tag
+    const uint32_t wend = mode == VM_RETAG ? (len > 16u ? len : 16u) : nlen;
+    const uint32_t nst = !act ? 0u : mode == VM_RETAG ? 1u : (wend + 15u) >> 4;  // chunks stored
+
+    uint4 nv[K];
+    vlan_edit<K>(nv, v, mode, rl, true, 0u, nx0, tag_dw, 0u, wend);
+    uint32_t carry = row_bcast<15, 16>(v[K - 1].w);  // push: old dword before batch 1
+
+    // update_checksums() on the edited frame (690 / 718)
+    RPlan P = fast_plan<R>(nv[0], rowbase4, nlen);
+    const bool slow = act && (P.st >> 8) != 0;
+    if (!act || slow) P = rplan_none(0);
+    const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
+    const uint32_t tailfix = P.flags & F_TAIL;
+    uint32_t rlv = rl;
+    asm volatile("" : "+v"(rlv));
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc_slot(acc, nv[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
+
+    // rows whose frame continues past batch 0 (moved chunks or summed chunks)
+    const uint32_t nre = (re + 15u) >> 4;
+    const uint32_t cm = (nst > nre) ? nst : nre;
+    const bool multi = __builtin_amdgcn_ballot_w64(cm > KR) != 0;  // wave-uniform
+    auto finish = [&](uint32_t a) -> uint32_t {  // l4 field word
+        const uint32_t z = row_sum<R>(a) + P.corr;
+        uint32_t c = (~fold32(z)) & 0xFFFFu;
+        if ((P.flags & F_UDP) && c == 0) c = 0xFFFFu;
+        return (P.flags & F_L4) ? (P.fs | (c << 16)) : NFCS_PATCH_NONE;
+    };
+    const uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
+    uint32_t l4w = NFCS_PATCH_NONE;
+    if (!multi) {
+        l4w = finish(acc);
+        // checksum bytes into the chunk registers (fast-path fields lie below byte 80: slot 0);
+        // a re-tag stores chunk 0 and the chunks holding checksum bytes
+        bool patched = false;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t w = (t < 2) ? ipw : l4w;
+            const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl) {
+                nv[0] = put_byte(nv[0], pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
+                patched = true;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rl + (uint32_t)R * k;
+            if (c < nst || (k == 0 && patched)) ((uint4*)frame)[c] = nv[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rl + (uint32_t)R * k;
+            if (c < nst) ((uint4*)frame)[c] = nv[k];
+        }
+        const uint32_t cmax = wave_max_rows<R>(cm);
+        for (uint32_t cb = KR; cb < cmax; cb += KR) {
+            uint4 w[K], e[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                w[k] = ld16<1>((c < nl) ? src + c : &g_zero16);
+            }
+            const uint32_t nx = *(const uint32_t*)((cb + KR < nl) ? src + cb + KR : &g_zero16);
+            vlan_edit<K>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
+            carry = row_bcast<15, 16>(w[K - 1].w);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                acc_slot(acc, e[k], c, lo4, re, tailfix);
+                if (c < nst) ((uint4*)frame)[c] = e[k];
+            }
+        }
+        l4w = finish(acc);
+        // the lanes that stored chunk pos/16 store the checksum bytes (program order)
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t w = (t < 2) ? ipw : l4w;
+            const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl)
+                frame[pos] = (uint8_t)(w >> (16 + 8 * (t & 1u)));
+        }
+    }
+    const uint32_t st0 = bad ? (uint32_t)NFCS_ST_BAD_DESC
+                       : mode == VM_FAIL ? (uint32_t)NFCS_ST_VLAN_FAIL
+                       : act ? (P.st | NFCS_ST_FLAG_VLAN) : (uint32_t)NFCS_ST_NONE;
+    if (valid && rl == 0) {
+        if (!slow && status) status[p] = (uint8_t)st0;
+        if (act) desc[p].len = nlen;
+    }
+    if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path on the edited frame in memory
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        RPlan Q = rplan_none(0);
+        SeqOut o = {0, 0, 0, 0, 0};
+        if (slow && rl == 0) {
+            Q = slow_plan(frame, nlen);
+            if (Q.flags & F_SEQ) o = seq_update(frame, nlen);
+        }
+        Q.st = row_bcast<0, R>(Q.st);
+        Q.flags = row_bcast<0, R>(Q.flags);
+        Q.ipw = row_bcast<0, R>(Q.ipw);
+        Q.rs = row_bcast<0, R>(Q.rs);
+        Q.re = row_bcast<0, R>(Q.re);
+        Q.fs = row_bcast<0, R>(Q.fs);
+        Q.corr = row_bcast<0, R>(Q.corr);
+        const uint32_t ost = row_bcast<0, R>(o.st);
+        const bool seq = slow && (Q.flags & F_SEQ);
+        const uint32_t re2 = (slow && !seq && (Q.flags & F_L4)) ? Q.re : 0u;
+        const uint32_t lo42 = Q.rs & ~3u, tf2 = Q.flags & F_TAIL;
+        uint32_t acc2 = 0;
+        for (uint32_t c = rl; c < ((re2 + 15u) >> 4); c += R) acc_slot(acc2, src[c], c, lo42, re2, tf2);
+        const uint32_t z2 = row_sum<R>(acc2) + Q.corr;
+        const uint32_t ipw2 = (Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE;
+        uint32_t l4w2 = NFCS_PATCH_NONE;
+        if (Q.flags & F_L4) {
+            uint32_t c = (~fold32(z2)) & 0xFFFFu;
+            if ((Q.flags & F_UDP) && c == 0) c = 0xFFFFu;
+            l4w2 = Q.fs | (c << 16);
+        }
+        if (slow && !seq && rl < 4) {
+            const uint32_t w = (rl & 2u) ? l4w2 : ipw2;
+            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+        }
+        if (slow && rl == 0 && status)
+            status[p] = (uint8_t)((seq ? (ost | NFCS_ST_FLAG_OVERLAP) : Q.st) | NFCS_ST_FLAG_VLAN);
+    }
+}
+
+hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
+                       uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream) {
+    (void)di;
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 15u) / 16u;  // 4 rows per wave, 4 waves per workgroup
+    hipLaunchKernelGGL((vlan_rows_kernel<6>), dim3(blocks), dim3(kBlock), 0, stream, arena,
+                       arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    return hipGetLastError();
+}
+
 // ---- flow-key extract + hash -----------------------------------------------
 // PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) on the first
 // 128 bytes of each frame: one 8-lane DPP row per packet (lane rl holds frame bytes

@@ -84,6 +84,11 @@ def lib() -> ctypes.CDLL:
         L.nfo_l3_forward_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, _u32p,
                                            ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p]
         L.nfo_l3_forward_batch.restype = ctypes.c_int
+        L.nfo_vlan.argtypes = [_u8p, _u32p, ctypes.c_uint32, ctypes.c_uint32]
+        L.nfo_vlan.restype = ctypes.c_int
+        L.nfo_vlan_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, _u32p, ctypes.c_uint32,
+                                     _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p]
+        L.nfo_vlan_batch.restype = ctypes.c_int
         L.nfo_flow_key.argtypes = [_u8p, ctypes.c_size_t, _u8p]
         L.nfo_flow_key.restype = ctypes.c_uint32
         L.nfo_flow_keys_batch.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
@@ -115,6 +120,11 @@ def ref() -> ctypes.CDLL:
         R.nfref_l3_forward_batch.argtypes = [_u8p, ctypes.c_void_p, _u32p, ctypes.c_uint32, _u8p,
                                              ctypes.c_uint32, ctypes.c_int]
         R.nfref_l3_forward_batch.restype = None
+        R.nfref_vlan.argtypes = [_u8p, _u32p, ctypes.c_uint32, ctypes.c_uint32]
+        R.nfref_vlan.restype = ctypes.c_int
+        R.nfref_vlan_batch.argtypes = [_u8p, ctypes.c_void_p, _u32p, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_int]
+        R.nfref_vlan_batch.restype = None
         R.nfref_flow_key.argtypes = [_u8p, ctypes.c_size_t, _u8p]
         R.nfref_flow_key.restype = ctypes.c_uint32
         R.nfref_flow_keys_batch.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint32, _u8p, _u32p,
@@ -165,6 +175,57 @@ def l3_forward_batch(arena: np.ndarray, desc: np.ndarray, nh_index: np.ndarray,
     lib().nfo_l3_forward_batch(_ptr(arena), arena.nbytes, desc.ctypes.data, _ptr(nh_index, _u32p),
                                n, _ptr(table) if table.size else None, table.size // 12,
                                _ptr(status))
+    return status
+
+
+VLAN_PUSH = 0x40000000
+VLAN_POP = 0x80000000
+
+
+def vlan_op(kind: str, vid: int = 0, prio: int = 0) -> int:
+    """Edit word of include/nfcs.h (NFCS_VLAN_OP): 'push' / 'pop' / 'nop'."""
+    k = {"push": VLAN_PUSH, "pop": VLAN_POP, "nop": 0}[kind]
+    return k | ((prio & 7) << 13) | (vid & 0xFFF) if k == VLAN_PUSH else k
+
+
+def vlan_window(n: int) -> int:
+    """Bytes of a frame's buffer an edit of an n-byte frame can touch: round_up(max(n+4, 16), 16)."""
+    return (max(n + 4, 16) + 15) // 16 * 16
+
+
+def _vlan_buf(frame: bytes, cap: int) -> np.ndarray:
+    size = max(cap, vlan_window(len(frame)))
+    return np.frombuffer(bytes(frame) + bytes(size - len(frame)), dtype=np.uint8).copy()
+
+
+def vlan_frame(frame: bytes, op: int, cap: int) -> tuple[bytes, int, bytes]:
+    """Oracle push_vlan/pop_vlan + update_checksums of one frame in a zero-filled buffer of
+    max(cap, vlan_window) bytes. Returns (new frame, status, buffer[:vlan_window(len)])."""
+    buf = _vlan_buf(frame, cap)
+    ln = np.array([len(frame)], dtype=np.uint32)
+    st = lib().nfo_vlan(_ptr(buf), _ptr(ln, _u32p), cap, op)
+    return bytes(buf[: int(ln[0])]), st, bytes(buf[: vlan_window(len(frame))])
+
+
+def ref_vlan_frame(frame: bytes, op: int, cap: int) -> tuple[bytes, int, bytes]:
+    """The reference's Packet::push_vlan / pop_vlan on the same buffer: (frame, ret, window)."""
+    buf = _vlan_buf(frame, cap)
+    ln = np.array([len(frame)], dtype=np.uint32)
+    ok = ref().nfref_vlan(_ptr(buf), _ptr(ln, _u32p), cap, op)
+    return bytes(buf[: int(ln[0])]), ok, bytes(buf[: vlan_window(len(frame))])
+
+
+def vlan_batch(arena: np.ndarray, desc: np.ndarray, ops=None, caps=None, op_all: int = 0,
+               cap_all: int = 0) -> np.ndarray:
+    """Oracle batch (nfcs_vlan_device contract): arena and desc lengths updated in place;
+    per-frame ops / caps arrays or uniform op_all / cap_all. Returns the status bytes."""
+    n = len(desc)
+    status = np.zeros(n, dtype=np.uint8)
+    o = None if ops is None else np.ascontiguousarray(ops, dtype=np.uint32)
+    c = None if caps is None else np.ascontiguousarray(caps, dtype=np.uint32)
+    lib().nfo_vlan_batch(_ptr(arena), arena.nbytes, desc.ctypes.data,
+                         None if o is None else _ptr(o, _u32p), op_all,
+                         None if c is None else _ptr(c, _u32p), cap_all, n, _ptr(status))
     return status
 
 
@@ -226,15 +287,16 @@ def fuzz_frames(seed: int, first: int, n: int) -> list[bytes]:
     return out
 
 
-def pack_frames(frames: list[bytes], align: int = 16):
-    """Lay frames out in one arena with `align`-byte starts (16-byte chunk padding)."""
+def pack_frames(frames: list[bytes], align: int = 16, room: int = 0):
+    """Lay frames out in one arena with `align`-byte starts (16-byte chunk padding); each slot
+    holds at least len + room bytes (room = 4 leaves tailroom for a VLAN push)."""
     assert align % 16 == 0
     n = len(frames)
     desc = np.zeros(n, dtype=DESC_DTYPE)
     off = 0
     for i, f in enumerate(frames):
         desc[i] = (off // 16, len(f))
-        off += (len(f) + align - 1) // align * align
+        off += (len(f) + room + align - 1) // align * align
     arena = np.zeros(max(off, 16), dtype=np.uint8)
     for i, f in enumerate(frames):
         o = int(desc[i]["off16"]) * 16

@@ -188,6 +188,74 @@ int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* d
     return 0;
 }
 
+/* ---- VLAN push / pop + checksum -------------------------------------------- */
+/* VlanHeader::set_vlan_id then set_priority (packet.hpp:185-190) on the TCI at bytes 14-15. */
+static void set_tci(uint8_t* f, unsigned vid, unsigned prio) {
+    unsigned tci = be16(f, 14);
+    tci = (tci & 0xF000u) | (vid & 0x0FFFu);
+    tci = (tci & 0x1FFFu) | ((prio & 7u) << 13);
+    store_be16(f, 14, (uint16_t)tci);
+}
+
+/* Packet::push_vlan(vid, prio) (packet.hpp:655-692) and pop_vlan() (694-720) on a frame whose
+ * buffer holds `cap` bytes from the frame start (the PacketBuffer's capacity minus headroom, so
+ * tailroom = cap - len). Frame bytes past the new length are left as the reference's memmove
+ * leaves them. */
+int nfo_vlan(uint8_t* f, uint32_t* len_io, uint32_t cap, uint32_t op) {
+    const uint32_t kind = op & NFO_VLAN_OP_MASK, vid = op & 0x0FFFu, prio = (op >> 13) & 7u;
+    uint32_t len = *len_io;
+    if (kind == NFO_VLAN_PUSH) {
+        if (len < 14) return NFO_ST_VLAN_FAIL;                         /* 656 */
+        if (be16(f, 12) == 0x8100) {                                   /* 661: has_vlan() */
+            set_tci(f, vid, prio);                                     /* 662-664: no bounds check */
+        } else {
+            if (len + 4 > cap) return NFO_ST_VLAN_FAIL;                /* 666-670 (headroom 0) */
+            memmove(f + 18, f + 14, len - 14);                         /* 673-676 */
+            f[16] = f[12];                                             /* 681: inner = original */
+            f[17] = f[13];
+            f[14] = 0;                                                 /* 679: tci = 0 */
+            f[15] = 0;
+            set_tci(f, vid, prio);                                     /* 679-680 */
+            f[12] = 0x81;                                              /* 683 */
+            f[13] = 0x00;
+            len += 4;                                                  /* 685 */
+        }
+    } else if (kind == NFO_VLAN_POP) {
+        if (len < 14 || be16(f, 12) != 0x8100) return NFO_ST_VLAN_FAIL; /* 695 */
+        if (len < 18) return NFO_ST_VLAN_FAIL;                          /* 698 */
+        const uint8_t e0 = f[16], e1 = f[17];                           /* 703 */
+        memmove(f + 14, f + 18, len - 18);                              /* 705-709 */
+        f[12] = e0;                                                     /* 711 */
+        f[13] = e1;
+        len -= 4;                                                       /* 713 */
+    } else {
+        return NFO_ST_NONE;                                             /* no edit requested */
+    }
+    *len_io = len;
+    return nfo_update(f, len) | NFO_ST_FLAG_VLAN;                       /* 690 / 718 */
+}
+
+int nfo_vlan_batch(uint8_t* arena, uint64_t arena_bytes, nfo_desc* desc, const uint32_t* ops,
+                   uint32_t op_all, const uint32_t* caps, uint32_t cap_all, uint32_t n,
+                   uint8_t* status) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t off = (uint64_t)desc[i].off16 * 16;
+        uint32_t len = desc[i].len;
+        const uint32_t op = ops ? ops[i] : op_all;
+        const uint32_t kind = op & NFO_VLAN_OP_MASK;
+        const uint64_t need = (uint64_t)len + (kind == NFO_VLAN_PUSH ? 4u : 0u);
+        int st;
+        if (off + ((need + 15) & ~15ull) > arena_bytes) {
+            st = NFO_ST_BAD_DESC;
+        } else {
+            st = nfo_vlan(arena + off, &len, caps ? caps[i] : cap_all, op);
+            desc[i].len = len;
+        }
+        if (status) status[i] = (uint8_t)st;
+    }
+    return 0;
+}
+
 /* ---- flow key ----------------------------------------------------------- */
 static inline void put16le(uint8_t* p, unsigned v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
 static inline void put32le(uint8_t* p, uint32_t v) {

@@ -25,8 +25,14 @@ enum {
     NFO_ST_NONE = 0, NFO_ST_V4 = 1, NFO_ST_V4_TCP = 2, NFO_ST_V4_UDP = 3, NFO_ST_V4_ICMP = 4,
     NFO_ST_V4_L4SKIP = 5, NFO_ST_V6 = 6, NFO_ST_V6_TCP = 7, NFO_ST_V6_UDP = 8,
     NFO_ST_V6_L4SKIP = 9, NFO_ST_NO_ROUTE = 11, NFO_ST_NOT_IPV4 = 12, NFO_ST_TTL_EXPIRED = 13,
-    NFO_ST_OOB = 14, NFO_ST_BAD_DESC = 15, NFO_ST_FLAG_OVERLAP = 0x40, NFO_ST_FLAG_FWD = 0x80
+    NFO_ST_OOB = 14, NFO_ST_BAD_DESC = 15, NFO_ST_VLAN_FAIL = 16, NFO_ST_FLAG_VLAN = 0x20,
+    NFO_ST_FLAG_OVERLAP = 0x40, NFO_ST_FLAG_FWD = 0x80
 };
+
+/* VLAN edit word (identical to include/nfcs.h NFCS_VLAN_*): op | prio << 13 | vid */
+#define NFO_VLAN_PUSH 0x40000000u
+#define NFO_VLAN_POP 0x80000000u
+#define NFO_VLAN_OP_MASK 0xC0000000u
 
 typedef struct nfo_desc { uint32_t off16; uint32_t len; } nfo_desc;
 
@@ -50,6 +56,18 @@ int nfo_l3_forward(uint8_t* frame, size_t len, const uint8_t* nh);
 int nfo_l3_forward_batch(uint8_t* arena, uint64_t arena_bytes, const nfo_desc* desc,
                          const uint32_t* nh_index, uint32_t n, const uint8_t* table,
                          uint32_t table_n, uint8_t* status);
+
+/* Packet::push_vlan(vid, prio) / pop_vlan() (packet.hpp:655-720) + their update_checksums()
+ * on one frame whose buffer holds cap bytes from the frame start. op = NFO_VLAN_PUSH | prio << 13
+ * | vid, NFO_VLAN_POP, or 0 (no edit). *len is updated. Returns NFO_ST_VLAN_FAIL when the
+ * reference returns false (frame untouched), NFO_ST_NONE for no edit, else the
+ * update_checksums() status | NFO_ST_FLAG_VLAN. The buffer must hold max(len + 4, 16) bytes. */
+int nfo_vlan(uint8_t* frame, uint32_t* len, uint32_t cap, uint32_t op);
+/* batch (the nfcs_vlan_device contract): op / cap of frame i = ops[i] / caps[i], or op_all /
+ * cap_all when the array is NULL; desc[i].len updated in place */
+int nfo_vlan_batch(uint8_t* arena, uint64_t arena_bytes, nfo_desc* desc, const uint32_t* ops,
+                   uint32_t op_all, const uint32_t* caps, uint32_t cap_all, uint32_t n,
+                   uint8_t* status);
 
 /* PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) of one frame,
  * written as the 64-byte nfcs_flow_key record of include/nfcs.h; returns the hash. */

@@ -177,6 +177,44 @@ __attribute__((visibility("default"))) void nfref_flow_keys_batch(uint8_t* arena
     for (auto& t : th) t.join();
 }
 
+// Packet::push_vlan(vid, prio) / pop_vlan() (packet.hpp:655-720), which end in
+// update_checksums(), on a frame whose PacketBuffer has `cap` bytes of capacity and no headroom
+// (tailroom = cap - len). op: bits 30-31 = 1 push / 2 pop, bits 13-15 priority, 0-11 VLAN id
+// (include/nfcs.h NFCS_VLAN_*). *len gets the buffer's new data length. Returns the reference's
+// bool (1 / 0), or -1 for no edit.
+__attribute__((visibility("default"))) int nfref_vlan(uint8_t* frame, uint32_t* len, uint32_t cap,
+                                                      uint32_t op) {
+    const uint32_t kind = op >> 30;
+    if (kind != 1 && kind != 2) return -1;
+    Window w;
+    w.point(frame, *len);
+    w.pb.capacity_ = cap;
+    netflow::Packet pkt(&w.pb);
+    const bool ok = kind == 1 ? pkt.push_vlan((uint16_t)(op & 0x0FFF), (uint8_t)((op >> 13) & 7))
+                              : pkt.pop_vlan();
+    *len = (uint32_t)w.pb.get_data_length();
+    return ok ? 1 : 0;
+}
+
+// Batch of the above over an arena (desc lengths updated) on `nthreads` std::threads: the CPU
+// baseline of the VLAN edit path.
+__attribute__((visibility("default"))) void nfref_vlan_batch(uint8_t* arena, void* desc_v,
+                                                             const uint32_t* ops, uint32_t n,
+                                                             uint32_t cap, int nthreads) {
+    Desc* desc = static_cast<Desc*>(desc_v);
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; ++i)
+            nfref_vlan(arena + (uint64_t)desc[i].off16 * 16, &desc[i].len, cap, ops[i]);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t)
+        th.emplace_back(work, (uint32_t)((uint64_t)n * t / nthreads),
+                        (uint32_t)((uint64_t)n * (t + 1) / nthreads));
+    work(0, (uint32_t)((uint64_t)n / nthreads));
+    for (auto& t : th) t.join();
+}
+
 __attribute__((visibility("default"))) int nfref_struct_sizes(int which) {
     switch (which) {
     case 0: return (int)sizeof(netflow::EthernetHeader);

@@ -17,6 +17,9 @@ reference does on:
   kat_flow.json     PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp,
   flow_ref.npz      compiled from the reference source) on builder-shaped frames and on fuzz
                     frames: 64-byte records (nfcs_flow_key layout) and hashes
+  kat_vlan.json     Packet::push_vlan / pop_vlan + update_checksums (packet.hpp:655-720) on
+  vlan_ref.npz      edit sequences over KAT frames and on fuzz frames with per-frame edits and
+                    buffer capacities: the buffer window after the edit, new length, return
 The fixtures are data only: frames in, frames/hashes out.
 """
 from __future__ import annotations
@@ -298,6 +301,146 @@ def make_flow(R):
           len(np.unique(hashes)), "distinct hashes")
 
 
+VLAN_SEED = 20250623
+VLAN_N = 32768
+
+
+def vlan_inputs(n=VLAN_N, seed=VLAN_SEED):
+    """Fuzz frames (25% tagged, IPv6, IHL 0-15, runts, jumbo) with one edit word and one buffer
+    capacity each: 40% push (random id / priority), 40% pop, 10% no edit, 10% push into a buffer
+    without tailroom; capacities len+4..len+68, exactly len+4, len..len+3 (no room) or 65536."""
+    frames = oracle.fuzz_frames(seed, 0, n)
+    rng = np.random.default_rng(seed)
+    ops = np.zeros(n, dtype=np.uint32)
+    caps = np.zeros(n, dtype=np.uint32)
+    for i, f in enumerate(frames):
+        r, c = rng.random(), rng.random()
+        vid, prio = int(rng.integers(0, 8192)), int(rng.integers(0, 8))
+        if r < 0.4 or r >= 0.9:
+            ops[i] = oracle.vlan_op("push", vid, prio)
+        elif r < 0.8:
+            ops[i] = oracle.vlan_op("pop")
+        ln = len(f)
+        if r >= 0.9 or c < 0.15:
+            caps[i] = ln + int(rng.integers(0, 4))
+        elif c < 0.65:
+            caps[i] = ln + 4 + int(rng.integers(0, 65))
+        elif c < 0.9:
+            caps[i] = ln + 4
+        else:
+            caps[i] = 65536
+    return frames, ops, caps
+
+
+def vlan_kat_frames():
+    """(name -> (frame, [ops], cap)): the reference's own push/pop uses (phase2_l2_parsing.cpp:114
+    push_vlan(202, 3) then pop_vlan(); packet_test.cpp:326-379 no tailroom / nothing to pop;
+    vlan_manager.cpp:90 ingress push of a native VLAN, :159/:174 egress pops) on the KAT frames,
+    plus runts, DEI preservation, IP options and IHL < 5 after the edit, and a jumbo frame."""
+    k = kat_frames()
+    P = lambda vid, prio=0: oracle.vlan_op("push", vid, prio)
+    POP = oracle.vlan_op("pop")
+    out = {}
+    for name in ("A_main_cpp_tcp", "B_packet_test_udp", "C_packet_test_tcp", "D_icmp_odd",
+                 "E_udp_odd_ABC", "G_udp_zero_to_ffff", "H1_icmp_all_zero", "I_ipv6_udp_data",
+                 "K_ipv4_ihl7_tcp", "M_ipv4_ihl2_udp_overlap"):
+        f = k[name]
+        out[f"{name}/push202p3_pop"] = (f, [P(202, 3), POP], len(f) + 4)
+        out[f"{name}/push_no_tailroom"] = (f, [P(10)], len(f))
+        out[f"{name}/pop_untagged"] = (f, [POP], len(f) + 64)
+    for name in ("F_vlan_udp", "J_ipv6_vlan_tcp"):
+        f = k[name]
+        out[f"{name}/pop"] = (f, [POP], len(f))
+        out[f"{name}/retag4095p7"] = (f, [P(4095, 7)], len(f))
+        out[f"{name}/pop_push1"] = (f, [POP, P(1, 0)], len(f))
+    dei = bytearray(k["F_vlan_udp"])
+    dei[14] |= 0x10  # DEI bit set: set_vlan_id / set_priority keep it (packet.hpp:185-190)
+    out["F_dei/retag7p2"] = (bytes(dei), [P(7, 2)], len(dei))
+    tag = bytes(12) + b"\x81\x00"
+    out["tagged_len14/retag"] = (tag, [P(0xABC, 5)], 14)  # writes TCI bytes 14-15 past len
+    out["tagged_len15/retag"] = (tag + b"\x42", [P(0x123, 1)], 15)
+    out["tagged_len17/pop"] = (tag + b"\x11\x22\x33", [POP], 17)
+    out["tagged_len18/pop"] = (tag + bytes.fromhex("e0010800"), [POP], 18)
+    out["untagged_len13/push"] = (bytes(12) + b"\x08", [P(5)], 64)
+    out["untagged_len14/push"] = (bytes(12) + b"\x08\x00", [P(5)], 18)
+    out["untagged_len14/push_cap17"] = (bytes(12) + b"\x08\x00", [P(5)], 17)
+    jumbo = oracle.gen_config(2, CONFIG_SEED, 7, 1)[0][:9000].tobytes()
+    out["C2_jumbo/push_pop"] = (jumbo, [P(300, 2), POP], 9004)
+    out["C2_jumbo/push"] = (jumbo, [P(300, 2)], 9004)
+    c1 = oracle.gen_config(1, CONFIG_SEED, 3, 1)[0][:1500].tobytes()
+    out["C1/push"] = (c1, [P(100, 6)], 1504)
+    odd = oracle.gen_config(3, CONFIG_SEED, 11, 1)
+    oddf = odd[0][:int(odd[1][0]["len"])].tobytes()
+    out["C3/push_pop"] = (oddf, [P(42), POP], len(oddf) + 4)
+    return out
+
+
+def make_vlan(R):
+    """VLAN push / pop + update_checksums (packet.hpp:655-720) through the reference's Packet."""
+    L = oracle.lib()
+    kats = {}
+    for name, (f, ops, cap) in vlan_kat_frames().items():
+        cur, rets, sts = f, [], []
+        buf_r = oracle._vlan_buf(f, cap)
+        buf_o = buf_r.copy()
+        ln_r = np.array([len(f)], dtype=np.uint32)
+        ln_o = ln_r.copy()
+        for op in ops:  # successive edits on the same buffer
+            rets.append(int(R.nfref_vlan(oracle._ptr(buf_r), oracle._ptr(ln_r, oracle._u32p), cap, op)))
+            sts.append(int(L.nfo_vlan(oracle._ptr(buf_o), oracle._ptr(ln_o, oracle._u32p), cap, op)))
+        w = oracle.vlan_window(len(f))
+        assert bytes(buf_r[:w]) == bytes(buf_o[:w]) and ln_r[0] == ln_o[0], name
+        assert all((s == 16) == (r == 0) for s, r in zip(sts, rets)), name
+        kats[name] = {"in": f.hex(), "ops": [int(o) for o in ops], "cap": int(cap),
+                      "out": bytes(buf_r[:w]).hex(), "len_out": int(ln_r[0]), "ret": rets,
+                      "status": sts}
+    with open(os.path.join(OUT, "kat_vlan.json"), "w") as fh:
+        json.dump(kats, fh, indent=1, sort_keys=True)
+    print("kat_vlan.json:", len(kats), "cases")
+    frames, ops, caps = vlan_inputs()
+    n = len(frames)
+    h_out = np.zeros(n, dtype=np.uint64)
+    len_out = np.zeros(n, dtype=np.uint32)
+    ret = np.zeros(n, dtype=np.int8)
+    st = np.zeros(n, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        o_orc, s, win_o = oracle.vlan_frame(f, int(ops[i]), int(caps[i]))
+        st[i] = s
+        if (s & 0x1F) == 14:  # IHL past the edited frame: the reference reads past it
+            continue
+        o, r, win = oracle.ref_vlan_frame(f, int(ops[i]), int(caps[i]))
+        assert win == win_o and o == o_orc and (r == 0) == (s == 16), i
+        ret[i] = r
+        len_out[i] = len(o)
+        wb = np.frombuffer(win, dtype=np.uint8).copy()
+        h_out[i] = L.nfo_frame_hash(oracle._ptr(wb), len(win))
+    np.savez_compressed(os.path.join(OUT, "vlan_ref.npz"), seed=np.uint64(VLAN_SEED), ops=ops,
+                        caps=caps, lens=np.array([len(f) for f in frames], dtype=np.uint16),
+                        len_out=len_out, ret=ret, hash_window=h_out, oracle_status=st)
+    print("vlan_ref.npz:", n, "frames; statuses", np.unique(st, return_counts=True))
+    # bench workload: C1 1M frames in 1536-byte slots, push_vlan(100, 3) then pop_vlan()
+    res = json.load(open(os.path.join(OUT, "configs.json")))
+    nb = 1 << 20
+    M = (1 << 64) - 1
+    d1 = d2 = 0
+    for lo in range(0, nb, CHUNK):
+        m = min(CHUNK, nb - lo)
+        arena, desc = oracle.gen_config(1, CONFIG_SEED, lo, m, 128)
+        R.nfref_vlan_batch(oracle._ptr(arena), desc.ctypes.data,
+                           oracle._ptr(np.full(m, oracle.vlan_op("push", 100, 3), np.uint32), oracle._u32p),
+                           m, 1536, 8)
+        d1 = (d1 + oracle.digest(arena, desc, lo)) & M
+        R.nfref_vlan_batch(oracle._ptr(arena), desc.ctypes.data,
+                           oracle._ptr(np.full(m, oracle.vlan_op("pop"), np.uint32), oracle._u32p),
+                           m, 1536, 8)
+        d2 = (d2 + oracle.digest(arena, desc, lo)) & M
+    res["vlan_c1"] = {"first": 0, "n": nb, "align": 128, "cap": 1536, "op_push": "push_vlan(100, 3)",
+                      "digest_push": f"{d1:016x}", "digest_push_pop": f"{d2:016x}"}
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+    print(f"vlan C1 digests push {d1:016x} push+pop {d2:016x}")
+
+
 def ref_config_digest(R, config, seed, first, n, nthreads=8):
     """Digest of config packets [first, first+n) before and after the REFERENCE."""
     din = dout = 0
@@ -339,7 +482,7 @@ def make_configs(R):
 if __name__ == "__main__":
     oracle.build(ref=True)
     R = oracle.ref()
-    what = sys.argv[1:] or ["kat", "fuzz", "configs", "l3", "flow"]
+    what = sys.argv[1:] or ["kat", "fuzz", "configs", "l3", "flow", "vlan"]
     if "kat" in what:
         make_kat(R)
     if "fuzz" in what:
@@ -350,3 +493,5 @@ if __name__ == "__main__":
         make_l3(R)
     if "flow" in what:
         make_flow(R)
+    if "vlan" in what:
+        make_vlan(R)

@@ -77,7 +77,7 @@ def test_status_codes_match_abi_header():
     ora = open(os.path.join(ROOT, "oracle", "nfcs_oracle.h")).read()
     abi = dict((m[0], int(m[1], 0)) for m in re.findall(r"NFCS_ST_(\w+)\s*=\s*(0x[0-9a-fA-F]+|\d+)", hdr))
     orc = dict((m[0], int(m[1], 0)) for m in re.findall(r"NFO_ST_(\w+)\s*=\s*(0x[0-9a-fA-F]+|\d+)", ora))
-    assert abi == orc and len(abi) == 17
+    assert abi == orc and len(abi) == 19
 
 
 def test_config_generator_and_layout(oracle_lib):
