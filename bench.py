@@ -159,6 +159,25 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
             run = lambda: L.nfo_flow_keys_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
                                                 oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p))
             threads = 1
+    elif op == "vlan":
+        # push_vlan(100, 3) / pop_vlan() alternately (each pass leaves the batch ready for the
+        # next), 1536-byte buffers: the frames are laid out 128-byte aligned as on the GPU
+        arena, desc = oracle.gen_config(config, SEED, 0, n, 128)
+        ops = [np.full(n, oracle.vlan_op("push", 100, 3), np.uint32),
+               np.full(n, oracle.vlan_op("pop"), np.uint32)]
+        flip = [0]
+        if kind == "reference":
+            R = oracle.ref()
+
+            def run():
+                R.nfref_vlan_batch(oracle._ptr(arena), desc.ctypes.data,
+                                   oracle._ptr(ops[flip[0]], oracle._u32p), n, 1536, threads)
+                flip[0] ^= 1
+        else:
+            def run():
+                oracle.vlan_batch(arena, desc, ops[flip[0]], None, cap_all=1536)
+                flip[0] ^= 1
+            threads = 1
     elif op == "l3fwd":
         g = golden_l3()
         table = np.frombuffer(bytes.fromhex(g["table"]), dtype=np.uint8).copy()
@@ -229,7 +248,7 @@ def main():
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--op", choices=["update", "l3fwd", "flowkey"], default="update")
+    ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -265,6 +284,21 @@ def main():
         algo_bytes = hdr + 76.0 * n
         step = lambda: eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
         regen = lambda: None
+    elif args.op == "vlan":
+        if args.config != 1:
+            raise SystemExit("--op vlan: config 1 (1536-byte buffers per 1500-byte frame)")
+        # push_vlan(100, 3) and pop_vlan() alternate, each on every frame; per packet the pass
+        # reads the frame, writes it back from byte 12 (moved by 4 bytes) and updates its length:
+        # push 2*len + 4 B, pop (len' = len + 4) 2*len' - 4 B; +8 B descriptor read, 4 B written
+        VPUSH, VCAP = nf.vlan_push_op(100, 3), 1536
+        flip = [0]
+
+        def step():
+            eng.vlan_device(d_arena, nbytes, d_desc, n, None, VPUSH if flip[0] == 0 else nf.VLAN_POP,
+                            None, VCAP)
+            flip[0] ^= 1
+        algo_bytes = 2.0 * frame_bytes + 4.0 * n + 12.0 * n
+        regen = lambda: step() if flip[0] else None  # back to untagged frames (pop)
     else:
         step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
         regen = lambda: None
@@ -306,6 +340,21 @@ def main():
         step()
         eng.sync()
         want = g3["digest_out"] if (args.config == 1 and first == 0 and n == g3["n"]) else None
+    elif args.op == "vlan":
+        regen()
+        ev_ms = eng.time_vlan_device(d_arena, nbytes, d_desc, n, VPUSH, nf.VLAN_POP, VCAP,
+                                     2 * ((args.steps + 1) // 2)) / (2 * ((args.steps + 1) // 2))
+        # parity: one push of the untagged batch vs the reference's digest, then one pop
+        gv = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json"))).get("vlan_c1", {})
+        on_ref = first == 0 and n == gv.get("n")
+        step()
+        eng.sync()
+        got_push = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
+        step()
+        eng.sync()
+        want = gv.get("digest_push_pop") if on_ref else golden_digest(1, first, n)
+        if on_ref and got_push != gv["digest_push"]:
+            want = "push digest " + gv["digest_push"] + " != " + got_push
     elif args.op == "flowkey":
         ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
                                           args.steps) / args.steps
@@ -325,7 +374,8 @@ def main():
     out = {
         "metric": ("flow keys + hash_flow per second, batched packets, MI355X" if fk else
                    "device-resident payload GB/s checksummed, batched packets, 1/2/4/8 MI355X"
-                   + (" (fused L3 forward: TTL--, MAC rewrite, checksums)" if l3 else "")),
+                   + (" (fused L3 forward: TTL--, MAC rewrite, checksums)" if l3 else "")
+                   + (" (VLAN push/pop + checksums)" if args.op == "vlan" else "")),
         "value": round(total_packets / (wall / args.steps) / 1e6, 2) if fk else
                  round(total_frame_bytes / (wall / args.steps) / 1e9, 2),
         "unit": "Mpkt/s" if fk else "GB/s",
@@ -339,7 +389,9 @@ def main():
         "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
         "config": {"workload": WORKLOAD[args.config] + (", fused L3 forward (next hop i % 9)" if l3 else "")
-                   + (", flow keys (header line only)" if fk else ""),
+                   + (", flow keys (header line only)" if fk else "")
+                   + (", push_vlan(100, 3) / pop_vlan() alternating, 1536-byte buffers"
+                      if args.op == "vlan" else ""),
                    "packets_per_gpu": n, "frame_align": args.align,
                    "frame_bytes_per_gpu": int(frame_bytes), "parallelism": f"independent shards x{ws}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
