@@ -4,9 +4,10 @@
 A "step" is one pass of the hot path — NetFlow++'s Packet::update_checksums()
 (packet.hpp:722-890), batched on the gfx950 engine — over one batch of synthetic frames that
 is already resident in HBM. At N=1 the workload is BASELINE config C1 (1 M x 1500 B IPv4+UDP
-on 1 MI355X); with --gpus N each rank owns its own C1 batch (packets [rank*n, (rank+1)*n)),
-so per-GPU work is fixed (weak scaling) and there is no collective on the data path: ranks
-only meet at the timing barriers.
+on 1 MI355X); with --gpus N > 1 it is BASELINE config C4 (32 M x 1500 B sharded across 8 GPUs):
+each rank owns its own batch of 4 M packets (packets [rank*n, (rank+1)*n)), so per-GPU work is
+fixed (weak scaling) and there is no collective on the data path: ranks only meet at the
+timing barriers.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1] [--packets n] [--no-cpu]
                   [--op update|l3fwd|flowkey]
@@ -39,12 +40,15 @@ import netflow_amd as nf  # noqa: E402
 SEED = 20250620
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip parameters)
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
+C4_PACKETS_PER_GPU = 1 << 22
 WORKLOAD = {
     0: "C0: 1024 x 64 B IPv4 (header checksum only)",
     1: "C1: 1M x 1500 B IPv4+UDP, device-resident",
     2: "C2: 1M x 9000 B IPv4+TCP jumbo, device-resident",
     3: "C3: 4M x U{64..1500} B IPv4 TCP/UDP mix, device-resident",
 }
+WORKLOAD_C4 = ("C4: 1500 B IPv4+UDP sharded as independent per-GPU batches, 4M packets per GPU "
+               "(32M over 8 GPUs), device-resident")
 
 
 def dist_env():
@@ -120,7 +124,7 @@ def golden_digest(config: int, first: int, n: int):
     if c and c["first"] == first and c["n"] == n:
         return c["digest_out"]
     if config == 1:
-        for sh in g.get("c1_rank_shards", []):
+        for sh in g.get("c1_rank_shards", []) + g.get("c4_rank_shards", []):
             if sh["first"] == first and sh["n"] == n:
                 return sh["digest_out"]
     return None
@@ -256,9 +260,13 @@ def main():
     ws, rank, local = dist_env()
     D = Dist(ws, rank, local)
     n = args.packets or DEFAULT_PACKETS[args.config]
+    c4 = ws > 1 and args.config == 1 and not args.packets
+    if c4:  # BASELINE C4: 32M x 1500 B over 8 GPUs = 4M packets per GPU (also at 2 and 4 GPUs)
+        n = C4_PACKETS_PER_GPU
     first, n = shard(rank, n)
 
-    eng = nf.Engine(local)
+    # NFCS_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a 1-GPU box
+    eng = nf.Engine(int(os.environ.get("NFCS_BENCH_DEVICE", local)))
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n, args.align)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
@@ -388,7 +396,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
-        "config": {"workload": WORKLOAD[args.config] + (", fused L3 forward (next hop i % 9)" if l3 else "")
+        "config": {"workload": (WORKLOAD_C4 if c4 else WORKLOAD[args.config])
+                   + (", fused L3 forward (next hop i % 9)" if l3 else "")
                    + (", flow keys (header line only)" if fk else "")
                    + (", push_vlan(100, 3) / pop_vlan() alternating, 1536-byte buffers"
                       if args.op == "vlan" else ""),

@@ -20,6 +20,7 @@ reference does on:
   kat_vlan.json     Packet::push_vlan / pop_vlan + update_checksums (packet.hpp:655-720) on
   vlan_ref.npz      edit sequences over KAT frames and on fuzz frames with per-frame edits and
                     buffer capacities: the buffer window after the edit, new length, return
+  configs.json      (c4) also the digests of the 8 C4 rank shards (4M x 1500 B each)
 The fixtures are data only: frames in, frames/hashes out.
 """
 from __future__ import annotations
@@ -479,6 +480,22 @@ def make_configs(R):
         json.dump(res, fh, indent=1, sort_keys=True)
 
 
+def make_c4(R):
+    """C4: 32M x 1500 B IPv4+UDP sharded across 8 GPUs, 4M packets per rank (weak scaling at
+    1/2/4/8 GPUs): the reference's digest of every rank's shard."""
+    res = json.load(open(os.path.join(OUT, "configs.json")))
+    shards = []
+    for r in range(8):
+        t = time.time()
+        din, dout = ref_config_digest(R, 1, CONFIG_SEED, r << 22, 1 << 22)
+        shards.append({"rank": r, "first": r << 22, "n": 1 << 22, "digest_in": f"{din:016x}",
+                       "digest_out": f"{dout:016x}"})
+        print(f"C4 shard {r}: {dout:016x} ({time.time() - t:.1f}s)")
+    res["c4_rank_shards"] = shards
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
     oracle.build(ref=True)
     R = oracle.ref()
@@ -495,3 +512,5 @@ if __name__ == "__main__":
         make_flow(R)
     if "vlan" in what:
         make_vlan(R)
+    if "c4" in what:
+        make_c4(R)

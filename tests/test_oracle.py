@@ -120,3 +120,14 @@ def test_reference_shim_cross_check():
         if (st & 0x3F) == 14:
             continue
         assert oracle.ref_update_frame(f) == o
+
+
+def test_c4_shard_digest_matches_reference(oracle_lib):
+    """BASELINE C4 (32M x 1500 B over 8 GPUs): the oracle's digest of rank 7's 4M-packet shard
+    equals the reference's (configs.json c4_rank_shards, tests/golden/make_golden.py c4)."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+    sh = g["c4_rank_shards"][7]
+    assert (sh["first"], sh["n"]) == (7 << 22, 1 << 22)
+    din, dout, _ = oracle.config_digest(1, 20250620, sh["first"], sh["n"], 8)
+    assert (f"{din:016x}", f"{dout:016x}") == (sh["digest_in"], sh["digest_out"])
