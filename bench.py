@@ -311,6 +311,10 @@ def main():
         step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
         regen = lambda: None
 
+    # torch (for the synchronize around the timed region) is imported and initialised before
+    # the warm-up: its first import takes ~1.5 s, and an idle GPU between warm-up and timed
+    # region re-enters the timed steps cold (rocprofv3 trace: C3 kernels 0.78 -> 0.99 ms)
+    device_sync()
     # untimed warm-up: W steps, continued until --warm-seconds have passed so the timed steps
     # run at the clock the GPU holds under this load (a cold start measured ~4% slower)
     tw = time.perf_counter()

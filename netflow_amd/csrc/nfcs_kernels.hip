@@ -568,7 +568,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
 // (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
-template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false>
+template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false, int SV = 0>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* patch, uint32_t table_n = 0) {
     const uint32_t len = S.len;
@@ -626,10 +626,55 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     uint32_t rlv = rl;
     asm volatile("" : "+v"(rlv));
     uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc_slot(acc, k == 0 ? h0 : S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
-    // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t nre = (re + 15u) >> 4;
+    if (SV == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc_slot(acc, k == 0 ? h0 : S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
+    } else {
+        // Sums without per-slot boundary branches: chunks below nre are added whole (the
+        // region starts below byte 80, in slot 0, where dwords under lo4 are masked); the last
+        // chunk's bytes past re and the odd trailing byte are corrected once per row by the
+        // lane that holds it. Frames longer than one batch leave their end to the masked
+        // continuation below.
+        const uint32_t last = nre - 1u, own = (re != 0) && (last < (uint32_t)R * K) && ((last & (R - 1)) == rl);
+        uint4 lc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint4 v = k == 0 ? h0 : S.v[k];
+            const uint32_t c = rlv + (uint32_t)R * k;
+            const uint32_t m = (c < nre) ? 0xFFFFFFFFu : 0u;
+            if (k == 0) {
+                const uint32_t o = 16u * c;
+                acc = wsum(v.x & m & ((o >= lo4) ? 0xFFFFFFFFu : 0u), acc);
+                acc = wsum(v.y & m & ((o + 4u >= lo4) ? 0xFFFFFFFFu : 0u), acc);
+                acc = wsum(v.z & m & ((o + 8u >= lo4) ? 0xFFFFFFFFu : 0u), acc);
+                acc = wsum(v.w & m & ((o + 12u >= lo4) ? 0xFFFFFFFFu : 0u), acc);
+            } else {
+                acc = wsum(v.w & m, wsum(v.z & m, wsum(v.y & m, wsum(v.x & m, acc))));
+            }
+            const bool sel = (last >> (R == 16 ? 4 : 3)) == (uint32_t)k;
+            lc.x = sel ? v.x : lc.x;
+            lc.y = sel ? v.y : lc.y;
+            lc.z = sel ? v.z : lc.z;
+            lc.w = sel ? v.w : lc.w;
+        }
+        if (own) {
+            const uint32_t o = 16u * last;
+            uint32_t ex = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int nb = (int)re - (int)(o + 4u * j);
+                const uint32_t mk = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
+                // bytes under lo4 of a one-chunk region were never added
+                const uint32_t ml = (o + 4u * j >= lo4) ? 0xFFFFFFFFu : 0u;
+                ex = wsum(comp(lc, j) & mk & ml, ex);
+            }
+            acc -= ex;
+            const uint32_t t = re - 1u;
+            if (tailfix) acc += 255u * ((comp(lc, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+        }
+    }
+    // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t cmax = wave_max_rows<R>(nre);
     for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
         uint4 w[K];
@@ -718,7 +763,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 
 // Grid-stride over packets (the default grid has one workgroup per 4*64/R packets, so no
 // loop), 64/R packet rows per wave.
-template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false>
+template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false, int SV = 0>
 __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
                                                                   uint64_t arena_bytes,
                                                                   const nfcs_desc* __restrict__ desc,
@@ -749,7 +794,7 @@ __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __res
         row_stage<K, NT, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
                                  rl, nh, &fa);
         if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-        row_process<K, NT, DBG, R, FWD>(S, rl, rowbase4, status, patch, fa.table_n);
+        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n);
     }
 }
 
@@ -779,12 +824,305 @@ __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restri
     }
 }
 
+// =============================================================================================
+// v4: lane-per-packet planning, row-per-packet summing.
+//
+// PMC (profiles/r01_pmc_per_packet.json) put v3 at ~103 VALU wave-instructions per packet, i.e.
+// ~65% of the VALU issue capacity on C1 and all of it on C3 (4 cycles per wave64 VALU op): the
+// per-packet header plan, executed by a 16-lane row, costs one wave instruction per four
+// packets. Here a wave owns P = 64 consecutive packets:
+//   phase A  lane j plans packet j alone: its 8-byte descriptor (one coalesced load for the
+//            wave), the first 80 header bytes in 20 registers (five 16-byte loads; an 802.1Q
+//            tag is one select per dword), then update_checksums()'s decisions at compile-time
+//            offsets, so one VALU instruction plans 64 packets. Uncommon headers call the
+//            lane-0-style slow planner (IP options) or the exact sequential emulation (IHL < 5)
+//            in their own lane. The plan goes to LDS as an 8-dword record.
+//   phase B  16-lane rows (four packets per wave instruction) stream the summed region of
+//            each packet exactly as v3 does (6 slots of 16-byte loads per lane, jumbo frames in
+//            further batches), the next four packets' record and loads in flight while the
+//            current four are summed, folded and written back.
+// =============================================================================================
+struct LaneHdr {  // view dwords of the first 80 frame bytes, 802.1Q tag removed for bytes >= 12
+    uint32_t d[20];
+    DEV uint32_t b(uint32_t o) const { return (d[o >> 2] >> (8 * (o & 3u))) & 0xFFu; }
+    DEV uint32_t le16(uint32_t o) const { return (d[o >> 2] >> (8 * (o & 2u))) & 0xFFFFu; }
+    DEV uint32_t be16(uint32_t o) const { return bswap16(le16(o)); }
+};
+
+// packet.hpp:773-889 in view coordinates for a compile-time l4 (34: IPv4 IHL 5, 54: IPv6).
+template <uint32_t L4>
+DEV RPlan lane_l4(const LaneHdr& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t proto, uint32_t sh) {
+    const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
+    uint32_t L = 0, st = 0, fl = F_L4, sub = (L4 & 2u) ? V.le16(L4 - 2) : 0u, fs = 0;
+    // sub: the LE word before an l4 at 2 mod 4 (sh = 4 keeps the parity) and the raw bytes of
+    // the checksum field the reference zeroes first (795 / 838 / 885)
+    auto field = [&](uint32_t FS, uint32_t re) {
+        uint32_t s = 0;
+        if (FS < re) s += V.b(FS) << ((FS & 1u) ? 8 : 0);
+        if (FS + 1 < re) s += V.b(FS + 1) << (((FS + 1) & 1u) ? 8 : 0);
+        return s;
+    };
+    if (proto == 6) {
+        if (L4 + 19 > lenv) { P.st = skip; return P; }  // sizeof(TcpHeader) == 19
+        const uint32_t hl = (V.b(L4 + 12) >> 4) * 4u;
+        if (v4) {
+            const uint32_t tl = V.be16(16);
+            if (tl < 20u) { P.st = skip; return P; }
+            L = (tl - 20u) & 0xFFFFu;
+        } else {
+            L = V.be16(18);
+        }
+        if (L < hl || L4 + L > lenv) { P.st = skip; return P; }
+        fs = L4 + 15;  // TcpHeader::checksum at offset 15 (19-byte packed struct)
+        sub += field(L4 + 15, L4 + L);
+        st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
+    } else if (proto == 17) {
+        if (L4 + 8 > lenv) { P.st = skip; return P; }
+        L = V.be16(L4 + 4);
+        if (L < 8 || L4 + L > lenv) { P.st = skip; return P; }
+        fs = L4 + 6;
+        sub += field(L4 + 6, L4 + L);
+        fl |= F_UDP;
+        st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
+    } else if (proto == 1 && v4) {
+        if (L4 + 8 > lenv) { P.st = skip; return P; }
+        const uint32_t tl = V.be16(16);
+        if (tl < 20u) { P.st = skip; return P; }
+        L = tl - 20u;
+        if (L4 + L > lenv || L < 8) { P.st = skip; return P; }
+        fs = L4 + 2;
+        sub += field(L4 + 2, L4 + L);
+        st = NFCS_ST_V4_ICMP;
+    } else {
+        return P;
+    }
+    uint32_t add = 0;
+    if (proto != 1) {  // pseudo-header in the LE domain (797-816 / 840-859)
+        add = bswap16(proto) + bswap16(L);
+        if (v4) {
+            add += V.le16(26) + V.le16(28) + V.le16(30) + V.le16(32);
+        } else {
+#pragma unroll
+            for (uint32_t w = 0; w < 32; w += 2) add += V.le16(22 + w);
+        }
+    }
+    const uint32_t re = L4 + L, t = re - 1;
+    if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
+    P.st = st;
+    P.flags |= fl;
+    P.rs = L4 + sh;
+    P.re = re + sh;
+    P.fs = fs + sh;
+    P.corr = add - sub;
+    return P;
+}
+
+// fast_plan on one lane's registers: h = frame dwords 0..19 (bytes >= len may hold anything).
+DEV RPlan lane_plan(const uint32_t (&h)[20], uint32_t len) {
+    const bool tagged = (len >= 14) && bswap16(h[3] & 0xFFFFu) == 0x8100u;  // ethernet(): l2 = 18
+    const uint32_t sh = tagged ? 4u : 0u;
+    LaneHdr V;
+#pragma unroll
+    for (int i = 0; i < 20; ++i) V.d[i] = (i < 3) ? h[i] : (i < 19 ? (tagged ? h[i + 1] : h[i]) : (tagged ? 0u : h[i]));
+    const uint32_t lenv = len - sh;
+    const uint32_t b0 = V.b(14);
+    if (len >= 14 + sh && lenv >= 34 && (b0 >> 4) == 4) {  // 728-734: IPv4 by nibble
+        if ((b0 & 15u) != 5) return rplan_none(NFCS_ST_NONE | (F_SEQ << 8));
+        // 739-740: header checksum, field (view 24-25) zeroed: LE words of view bytes 14..33
+        uint32_t s = (V.d[3] >> 16) + (V.d[8] & 0xFFFFu);
+        s = wsum(V.d[4], wsum(V.d[5], wsum(V.d[6] & 0xFFFF0000u, wsum(V.d[7], s))));
+        RPlan P = rplan_none(NFCS_ST_V4);
+        P.flags = F_IP;
+        P.ipw = (24u + sh) | (((~fold32(s)) & 0xFFFFu) << 16);
+        return lane_l4<34>(V, P, lenv, 1u, V.b(23), sh);
+    }
+    // 741-765: effective EtherType (after one tag) must be IPv6 and the nibble 6
+    const uint32_t et = (len >= 14 + sh) ? V.be16(12) : 0u;
+    if (et != 0x86DDu || !(len >= 14 + sh && lenv >= 54 && (b0 >> 4) == 6))
+        return rplan_none(NFCS_ST_NONE);
+    return lane_l4<54>(V, rplan_none(NFCS_ST_V6), lenv, 0u, V.b(20), sh);
+}
+
+// Plan record in LDS, 8 dwords per packet.
+enum : uint32_t { RF_LIVE = 1u << 29, RF_DONE = 1u << 30 };  // in r[1] with flags << 24
+struct LRec { uint32_t off16, re_fl, rs_fs, corr, ipw, st, l4w, pad; };
+
+template <int P>
+struct LpShared { uint4 rec[kWavesPerBlock][P][2]; };
+
+template <int K, int R, int P, int DBG>
+__global__ __launch_bounds__(kBlock, 1) void update_lp_kernel(uint8_t* __restrict__ arena,
+                                                              uint64_t arena_bytes,
+                                                              const nfcs_desc* __restrict__ desc,
+                                                              uint32_t n, uint32_t base16,
+                                                              uint8_t* __restrict__ status,
+                                                              nfcs_patch* __restrict__ patch) {
+    static_assert(P == 64, "one plan lane per packet");
+    __shared__ LpShared<P> sh;
+    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
+    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * P;
+    if (pw >= n) return;
+    // ---- phase A: lane `lane` plans packet pw + lane -----------------------------------------
+    {
+        const uint64_t p = pw + lane;
+        const bool valid = p < n;
+        const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
+        const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
+        const bool bad = valid && ((d.off16 < base16) ||
+                                   (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
+        const bool live = valid && !bad;
+        const uint32_t len = live ? d.len : 0u;
+        uint8_t* frame = arena + (live ? off : 0);
+        const uint32_t nch = (len + 15u) >> 4;
+        uint32_t h[20];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint4 c = ld16<0>(((uint32_t)k < nch) ? (const uint4*)frame + k : &g_zero16);
+            h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
+        }
+        RPlan Q = lane_plan(h, len);
+        uint32_t l4w = NFCS_PATCH_NONE, done = 0;
+        if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
+            Q = slow_plan(frame, len);
+            if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
+                const SeqOut o = seq_update(frame, len);
+                Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
+                Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
+                l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
+                done = RF_DONE;
+            }
+        }
+        if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
+        const uint32_t re = (Q.flags & F_L4) ? Q.re : 0u;
+        // phase B sums whole chunks from chunk 0: the frame dwords below lo4 = rs & ~3 (all in
+        // h: rs <= l2 + 60 < 80) are subtracted here once, so no chunk needs a start mask
+        {
+            const uint32_t lo4 = Q.rs & ~3u;
+            uint32_t hs = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 20; ++q) hs = wsum((4u * q < lo4) ? h[q] : 0u, hs);
+            if (re) Q.corr -= hs;
+        }
+        const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
+        uint4* r = sh.rec[wv][lane];
+        r[0] = make_uint4(live ? (uint32_t)(off >> 4) : 0u, re | (Q.flags << 24) | (valid ? RF_LIVE : 0u) | done,
+                          (Q.rs & 0xFFFFu) | (Q.fs << 16), Q.corr);
+        r[1] = make_uint4(ipw, Q.st, l4w, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // ---- phase B: rows of R lanes sum their packet's region --------------------------------
+    constexpr uint32_t PR = 64 / R;  // packets per wave instruction
+    const uint32_t rl = lane & (R - 1), row = lane / R;
+    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
+    const uint32_t iters = (cnt + PR - 1) / PR;
+
+    struct Stage {
+        uint4 v[K];
+        uint4 t;   // the region's last chunk (end excess, odd-tail byte)
+        uint4 r0;  // off16, re | flags, rs | fs, corr (header prefix folded in)
+        uint32_t idx;
+    };
+    auto stage = [&](Stage& S, uint32_t it) {
+        // rlv is opaque in every iteration, so per-slot offsets are recomputed rather than
+        // hoisted out of the loop into long-lived VGPRs
+        uint32_t rlv = rl;
+        asm volatile("" : "+v"(rlv));
+        S.idx = it * PR + row;
+        S.r0 = sh.rec[wv][S.idx][0];
+        const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
+        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
+        // chunks 0 .. nre-1 in full (chunks past the region read zeros)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rlv + (uint32_t)R * k;
+            const uint4* a = (c < nre) ? src + c : &g_zero16;
+            S.v[k] = (k == 0) ? ld16<0>(a) : ld16<1>(a);
+        }
+        S.t = ld16<0>(nre ? src + (nre - 1u) : &g_zero16);
+    };
+    auto finish = [&](const Stage& S) {
+        uint32_t rlv = rl;
+        asm volatile("" : "+v"(rlv));
+        const uint32_t fl = (S.r0.y >> 24) & 0x1Fu;
+        const uint32_t re = S.r0.y & 0x1FFFFu, fs = S.r0.z >> 16;
+        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = add_chunk(S.v[k], acc);
+        const uint32_t nre = (re + 15u) >> 4;
+        const uint32_t cmax = wave_max_rows<R>(nre);
+        // jumbo frames: the rest in batches of K2 slots (the next stage's K slots are in flight,
+        // so a K-slot batch here would cost 30 VGPRs for the whole kernel)
+        constexpr int K2 = 2;
+        for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K2) {
+            uint4 w[K2];
+#pragma unroll
+            for (int k = 0; k < K2; ++k) {
+                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
+            }
+#pragma unroll
+            for (int k = 0; k < K2; ++k) acc = add_chunk(w[k], acc);
+        }
+        if (rl == 0 && re) {  // the last chunk's bytes past re; the odd trailing byte (903-905)
+            const uint32_t o = (re - 1u) & ~15u;
+            uint32_t ex = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int nb = (int)re - (int)(o + 4u * j);
+                const uint32_t m = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
+                ex = wsum(comp(S.t, j) & m, ex);
+            }
+            acc -= ex;
+            const uint32_t t = re - 1u;
+            if (fl & F_TAIL) acc += 255u * ((comp(S.t, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+        }
+        const uint32_t z = row_sum<R>(acc) + S.r0.w;
+        const uint4 r1 = sh.rec[wv][S.idx][1];
+        const bool done = S.r0.y & RF_DONE, live = S.r0.y & RF_LIVE;
+        uint32_t l4w = r1.z;
+        if (!done && (fl & F_L4)) {
+            uint32_t c = (~fold32(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
+            if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
+            l4w = fs | (c << 16);
+        }
+        const uint32_t ipw = r1.x;
+        uint8_t* frame = arena + (uint64_t)S.r0.x * 16u;
+        if (!(DBG & 1) && live && !done && rl < 4) {
+            const uint32_t w = (rl & 2u) ? l4w : ipw;
+            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+        }
+        if (live && rl == 0) {
+            const uint64_t p = pw + S.idx;
+            if (status) status[p] = (uint8_t)r1.y;
+            if (patch) {
+                uint2 pr;
+                pr.x = (ipw & 0xFFFFu) | (l4w << 16);
+                pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
+                ((uint2*)patch)[p] = pr;
+            }
+        }
+    };
+    Stage A, B;
+    stage(A, 0);
+    for (uint32_t it = 0; it < iters; it += 2) {
+        if (it + 1 < iters) stage(B, it + 1);
+        finish(A);
+        if (it + 1 >= iters) break;
+        if (it + 2 < iters) stage(A, it + 2);
+        finish(B);
+    }
+}
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, hipStream_t stream, int variant, int grid,
                          const Work& work) {
     nfcs_patch* ws = work.patch;
     if (n == 0) return hipSuccess;
+    if (variant == 0 && use_split(0, arena_bytes, n)) variant = 8;  // large frames: split mode
     // One workgroup per 4*64/R packets, as many workgroups as that takes (a grid that
     // grid-strides over resident workgroups measured 10-15% slower: DESIGN.md §5).
     auto rows_grid = [&](int R) {
@@ -798,17 +1136,46 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                        0, stream, arena, arena_bytes, desc, n, base16, status, PP, nofwd)
 #define NFCS_ROWSP(K, NT, R, DBG, PP) NFCS_ROWSO(K, NT, R, DBG, 1, PP)
 #define NFCS_ROWS(K, NT, R) NFCS_ROWSP(K, NT, R, 0, patch)
+#define NFCS_LP(K, R, DBG, PP)                                                                    \
+    hipLaunchKernelGGL((update_lp_kernel<K, R, 64, DBG>), dim3((n + 255u) / 256u), dim3(kBlock), 0, \
+                       stream, arena, arena_bytes, desc, n, base16, status, PP)
     switch (variant) {
     default:
-    case 0: NFCS_ROWS(6, 2, 16); break;   // 16-lane rows; header slot cached, payload evict-first
+    case 0:  // 16-lane rows; header slot cached, payload evict-first; branch-free sums
+    case 24: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1>), dim3(rows_grid(16)),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;
+    case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
     case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
     case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
     case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
     case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
+    case 25: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8-lane rows K=6, branch-free sums
+    case 26: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8-lane rows K=12, branch-free sums
+    case 20: NFCS_LP(6, 16, 0, patch); break;  // v4: lane plans, 16-lane row sums
+    case 21: NFCS_LP(6, 8, 0, patch); break;   // v4: lane plans, 8-lane row sums
+    case 22:
+    case 23: {  // v4 split: checksum pass without frame stores, then the patch pass
+        nfcs_patch* pp = patch ? patch : ws;
+        if (!pp) return hipErrorInvalidValue;
+        if (variant == 22) NFCS_LP(6, 16, 1, pp);
+        else NFCS_LP(6, 8, 1, pp);
+        int ga = (int)((n + kBlock - 1) / kBlock);
+        if (ga > di.cus * 8) ga = di.cus * 8;
+        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+                           base16, pp);
+        break;
+    }
     case 8: {  // split: checksum pass without frame stores, then the patch pass
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
-        NFCS_ROWSP(6, 2, 16, 1, pp);
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
+                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
+                           nofwd);
         int ga = (int)((n + kBlock - 1) / kBlock);
         if (ga > di.cus * 8) ga = di.cus * 8;
         hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
@@ -826,8 +1193,12 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 142: NFCS_ROWSP(6, 2, 16, 8, patch); break;  // high priority load issue
     case 155: NFCS_ROWS(12, 1, 8); break;      // 8-lane rows, all loads evict-first
     case 156: NFCS_ROWS(8, 2, 8); break;       // 8-lane rows, 8 slots
+    case 157: NFCS_ROWS(6, 2, 8); break;       // 8-lane rows, 6 slots (768 B per batch)
+    case 158: NFCS_ROWS(4, 2, 8); break;       // 8-lane rows, 4 slots
+    case 159: NFCS_ROWSP(6, 2, 8, 1, patch); break;  // 8-lane rows, 6 slots, no frame stores
 #endif
     }
+#undef NFCS_LP
 #undef NFCS_ROWS
 #undef NFCS_ROWSP
 #undef NFCS_ROWSO

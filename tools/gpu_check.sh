@@ -18,6 +18,11 @@ for cfg in 1 2 3; do
   rc=$?; echo "bench c$cfg rc=$rc"; cat "$OUT/bench_c$cfg.json"; [ $rc -eq 0 ] || exit $rc
 done
 
+for op in l3fwd flowkey vlan; do
+  timeout -k 10 300 python bench.py --op $op --steps 20 --warmup 3 --no-cpu > "$OUT/bench_$op.json" 2> "$OUT/bench_$op.err"
+  rc=$?; echo "bench $op rc=$rc"; cat "$OUT/bench_$op.json"; [ $rc -eq 0 ] || exit $rc
+done
+
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o c1 -- \
   python3 bench.py --config 1 --steps 20 --warmup 3 --no-cpu > "$OUT/prof_c1.log" 2>&1
