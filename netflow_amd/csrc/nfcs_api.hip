@@ -150,6 +150,7 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     c->di.cus = prop.multiProcessorCount;
     strncpy(c->di.arch, prop.gcnArchName, sizeof(c->di.arch) - 1);
     c->variant = env_int("NFCS_VARIANT", 0);
+    c->di.lds_pad = (unsigned)env_int("NFCS_LDS_PAD", 0);
     c->grid = env_int("NFCS_GRID", 0);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_digest, sizeof(uint64_t));
@@ -224,7 +225,7 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
-                               cap_all, d_status, pick(c, stream)));
+                               cap_all, d_status, pick(c, stream), c->variant));
     return NFCS_OK;
 }
 
@@ -461,7 +462,8 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
-                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st));
+                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
+                                   c->variant));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

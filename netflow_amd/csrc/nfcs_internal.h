@@ -25,6 +25,9 @@ struct DevInfo {
     int device = 0;
     int cus = 256;
     char arch[64] = {0};
+    // measurement knob (env NFCS_LDS_PAD): dynamic LDS bytes per workgroup, which caps the
+    // workgroups per CU and so the waves per SIMD; 0 in production
+    unsigned lds_pad = 0;
 };
 
 // Per-context device workspace handed to the checksum launch.
@@ -58,7 +61,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream);
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, int variant = 0);
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,

@@ -1143,7 +1143,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     default:
     case 0:  // 16-lane rows; header slot cached, payload evict-first; branch-free sums
     case 24: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1>), dim3(rows_grid(16)),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                dim3(kBlock), di.lds_pad, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;
     case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
     case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
@@ -1300,7 +1300,7 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K>
+template <int K, int K2 = 2>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1421,18 +1421,21 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             if (c < nst) ((uint4*)frame)[c] = nv[k];
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
-        for (uint32_t cb = KR; cb < cmax; cb += KR) {
-            uint4 w[K], e[K];
+        // the rest of a long frame in batches of K2 slots (K2 < K saves VGPRs: w and e live
+        // together here)
+        constexpr uint32_t KR2 = (uint32_t)(K2 * R);
+        for (uint32_t cb = KR; cb < cmax; cb += KR2) {
+            uint4 w[K2], e[K2];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
+            for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 w[k] = ld16<1>((c < nl) ? src + c : &g_zero16);
             }
-            const uint32_t nx = *(const uint32_t*)((cb + KR < nl) ? src + cb + KR : &g_zero16);
-            vlan_edit<K>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
-            carry = row_bcast<15, 16>(w[K - 1].w);
+            const uint32_t nx = *(const uint32_t*)((cb + KR2 < nl) ? src + cb + KR2 : &g_zero16);
+            vlan_edit<K2>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
+            carry = row_bcast<15, 16>(w[K2 - 1].w);
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
+            for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
                 if (c < nst) ((uint4*)frame)[c] = e[k];
@@ -1496,12 +1499,18 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream) {
-    (void)di;
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, int variant) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + 15u) / 16u;  // 4 rows per wave, 4 waves per workgroup
-    hipLaunchKernelGGL((vlan_rows_kernel<6>), dim3(blocks), dim3(kBlock), 0, stream, arena,
-                       arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD). Batches of 2 slots
+    // (variant 31: 94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, and capping the
+    // occupancy lower with LDS padding slower still (profiles/r01_s2_occupancy.md).
+    if (variant == 31)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 2>), dim3(blocks), dim3(kBlock), di.lds_pad, stream, arena,
+                           arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    else
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6>), dim3(blocks), dim3(kBlock), di.lds_pad, stream, arena,
+                           arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     return hipGetLastError();
 }
 
