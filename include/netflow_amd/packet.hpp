@@ -9,7 +9,10 @@
 //   netflow_amd::update_checksums_batch(Packet* const*, size_t)
 // which gathers the frames into a pinned, 16-byte-aligned arena, runs the gfx950 engine
 // through the C ABI (include/nfcs.h), copies back 8-byte patch records and writes the 2+2
-// checksum bytes into each PacketBuffer in place — bit-exact with the reference.
+// checksum bytes into each PacketBuffer in place — bit-exact with the reference; and
+// Packet::push_vlan / pop_vlan (packet.hpp:655-720) with their batched form
+//   netflow_amd::vlan_batch(Packet* const*, const uint32_t* ops, size_t, bool* ok)
+// (nfcs_vlan_device: tag insert / strip / re-tag and the checksums in one pass).
 //
 // All checksum arithmetic happens on the GPU; there is no CPU fallback. Constructing the
 // engine without a gfx950 device throws std::runtime_error ("fail loudly").
@@ -126,6 +129,14 @@ public:
     // status (optional) receives one NFCS_ST_* byte per packet. Returns 0 or an NFCS_E* code.
     inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr);
 
+    // Batched Packet::push_vlan(vid, prio) / pop_vlan() (packet.hpp:655-720), each with the
+    // update_checksums() it ends with. ops[i] is an NFCS_VLAN_* edit word (NFCS_VLAN_PUSH_OP(vid,
+    // prio), NFCS_VLAN_POP or NFCS_VLAN_NOP); ok[i] (optional) receives what the reference call
+    // returns; each PacketBuffer's data length changes as the reference changes it. The buffer's
+    // room for a push is its capacity minus headroom (tailroom = that minus the length).
+    inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
+                          uint8_t* status = nullptr);
+
     nfcs_ctx* ctx() const { return ctx_; }
 
 private:
@@ -137,7 +148,10 @@ private:
         if (d_desc_) nfcs_device_free(ctx_, d_desc_);
         if (d_patch_) nfcs_device_free(ctx_, d_patch_);
         if (d_status_) nfcs_device_free(ctx_, d_status_);
+        if (h_ops_) nfcs_host_free(ctx_, h_ops_);
+        if (d_ops_) nfcs_device_free(ctx_, d_ops_);
         h_arena_ = h_desc_ = h_patch_ = d_arena_ = d_desc_ = d_patch_ = d_status_ = nullptr;
+        h_ops_ = d_ops_ = nullptr;
         arena_cap_ = pkt_cap_ = 0;
     }
     int reserve(size_t arena_bytes, size_t n) {
@@ -153,6 +167,8 @@ private:
         if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_ * sizeof(nfcs_desc), &d_desc_);
         if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_ * sizeof(nfcs_patch), &d_patch_);
         if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_, &d_status_);
+        if (!rc) rc = nfcs_host_alloc(ctx_, pkt_cap_ * 2 * sizeof(uint32_t), &h_ops_);  // ops, caps
+        if (!rc) rc = nfcs_device_alloc(ctx_, pkt_cap_ * 2 * sizeof(uint32_t), &d_ops_);
         if (rc) release();
         return rc;
     }
@@ -161,6 +177,7 @@ private:
     std::mutex mu_;
     void *h_arena_ = nullptr, *h_desc_ = nullptr, *h_patch_ = nullptr;
     void *d_arena_ = nullptr, *d_desc_ = nullptr, *d_patch_ = nullptr, *d_status_ = nullptr;
+    void *h_ops_ = nullptr, *d_ops_ = nullptr;
     size_t arena_cap_ = 0, pkt_cap_ = 0;
 };
 
@@ -188,6 +205,13 @@ public:
 
     PacketBuffer* get_buffer() const { return buffer_; }
 
+    // packet.hpp:655 / 694, through the engine as a batch of one (each ends with
+    // update_checksums(), like the reference). Return what the reference returns.
+    bool push_vlan(uint16_t vlan_id_val, uint8_t priority = 0) {
+        return vlan_edit(NFCS_VLAN_PUSH_OP(vlan_id_val, priority));
+    }
+    bool pop_vlan() { return vlan_edit(NFCS_VLAN_POP); }
+
     // packet.hpp:722. Single packets go through the same GPU engine as a batch of one (a
     // latency-bound use; batch with update_checksums_batch). void, like the reference.
     void update_checksums() {
@@ -198,6 +222,15 @@ public:
     }
 
 private:
+    bool vlan_edit(uint32_t op) {
+        if (!buffer_) return false;
+        Packet* self = this;
+        bool ok = false;
+        const int rc = ChecksumEngine::instance().vlan_batch(&self, &op, 1, &ok);
+        if (rc != NFCS_OK) throw std::runtime_error(std::string("vlan edit: ") + nfcs_strerror(rc));
+        return ok;
+    }
+
     PacketBuffer* buffer_;
 };
 
@@ -248,12 +281,83 @@ inline int ChecksumEngine::update_checksums_batch(Packet* const* pkts, size_t n,
     return NFCS_OK;
 }
 
+inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok,
+                                      uint8_t* status) {
+    if (n == 0) return NFCS_OK;
+    if (!pkts || !ops || n > 0xFFFFFFFFu) return NFCS_EINVAL;
+    std::lock_guard<std::mutex> lock(mu_);
+    // gather: each frame in a slot of round_up(len + 4, 16) bytes (room for a pushed tag)
+    auto slot = [](size_t len) { return (len + 4 + 15) & ~size_t(15); };
+    size_t bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        bytes += slot(b ? b->get_data_length() : 0);
+    }
+    if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
+    int rc = reserve(bytes + 16, n);
+    if (rc) return rc;
+    uint8_t* arena = static_cast<uint8_t*>(h_arena_);
+    nfcs_desc* desc = static_cast<nfcs_desc*>(h_desc_);
+    uint32_t* hops = static_cast<uint32_t*>(h_ops_);
+    uint32_t* hcaps = hops + pkt_cap_;
+    size_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        const size_t len = b ? b->get_data_length() : 0;
+        if (len) std::memcpy(arena + off, b->get_data_start_ptr(), len);
+        // bytes past the frame: the buffer's own bytes where it has them (a re-tag of a runt
+        // writes bytes 14-15 past len, a pop leaves its last 4 bytes), zeros otherwise
+        const size_t have = b ? b->get_capacity() - b->get_headroom() : 0;
+        const size_t tail = slot(len) - len, keep = have > len ? (have - len < tail ? have - len : tail) : 0;
+        if (keep) std::memcpy(arena + off + len, b->get_data_start_ptr() + len, keep);
+        std::memset(arena + off + len + keep, 0, tail - keep);
+        desc[i] = nfcs_desc{static_cast<uint32_t>(off >> 4), static_cast<uint32_t>(len)};
+        hops[i] = b ? ops[i] : NFCS_VLAN_NOP;
+        hcaps[i] = static_cast<uint32_t>(have < 0xFFFFFFFFu ? have : 0xFFFFFFFFu);
+        off += slot(len);
+    }
+    const uint32_t m = static_cast<uint32_t>(n);
+    uint32_t* dops = static_cast<uint32_t*>(d_ops_);
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_arena_, arena, off))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_desc_, desc, n * sizeof(nfcs_desc)))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, dops, hops, n * sizeof(uint32_t)))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, dops + pkt_cap_, hcaps, n * sizeof(uint32_t)))) return rc;
+    if ((rc = nfcs_vlan_device(ctx_, static_cast<uint8_t*>(d_arena_), off,
+                               static_cast<nfcs_desc*>(d_desc_), m, dops, 0, dops + pkt_cap_, 0,
+                               static_cast<uint8_t*>(d_status_), nullptr)))
+        return rc;
+    if ((rc = nfcs_memcpy_d2h(ctx_, arena, d_arena_, off))) return rc;
+    std::vector<nfcs_desc> nd(n);
+    if ((rc = nfcs_memcpy_d2h(ctx_, nd.data(), d_desc_, n * sizeof(nfcs_desc)))) return rc;
+    std::vector<uint8_t> st(n);
+    if ((rc = nfcs_memcpy_d2h(ctx_, st.data(), d_status_, n))) return rc;
+    // scatter: the edited window back into each PacketBuffer and its new data length
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        const bool done = (st[i] & NFCS_ST_FLAG_VLAN) != 0;
+        if (ok) ok[i] = done;
+        if (status) status[i] = st[i];
+        if (!b || !done) continue;
+        const size_t len = desc[i].len, nlen = nd[i].len;
+        const size_t have = b->get_capacity() - b->get_headroom();
+        size_t w = len > nlen ? len : nlen;
+        if (w < 16 && have >= 16) w = 16;  // re-tag of a runt: TCI bytes 14-15
+        std::memcpy(b->get_data_start_ptr(), arena + (size_t)desc[i].off16 * 16, w < have ? w : have);
+        b->set_data_len(nlen);
+    }
+    return NFCS_OK;
+}
+
 // Free-function form on the process-wide engine.
 inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr) {
     return ChecksumEngine::instance().update_checksums_batch(pkts, n, status);
 }
 inline int update_checksums_batch(const std::vector<Packet*>& pkts, uint8_t* status = nullptr) {
     return update_checksums_batch(pkts.data(), pkts.size(), status);
+}
+inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
+                      uint8_t* status = nullptr) {
+    return ChecksumEngine::instance().vlan_batch(pkts, ops, n, ok, status);
 }
 
 }  // namespace netflow_amd

@@ -3,6 +3,10 @@
 //   cpu     : PacketBuffer / Packet semantics; engine construction must fail loudly w/o GPU
 //   batch   : update_checksums_batch over all frames; prints "<status> <hex>" per frame
 //   single  : Packet::update_checksums() per frame; prints "<hex>" per frame
+//   vlan    : lines "<op> <room> <hex>"; vlan_batch over all frames in zero-filled buffers with
+//             `room` bytes from the data start; prints "<ok> <status> <new len> <hex of room
+//             bytes from the data start>" per frame
+//   vlan1   : same through Packet::push_vlan / pop_vlan one packet at a time
 #include <netflow_amd/packet.hpp>
 
 #include <cstdio>
@@ -46,9 +50,49 @@ static int cpu_checks() {
     return bad;
 }
 
+static int vlan_mode(bool single) {
+    std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
+    std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
+    std::vector<uint32_t> ops, room;
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        const size_t a = line.find(' '), b = line.find(' ', a + 1);
+        ops.push_back((uint32_t)std::stoul(line.substr(0, a)));
+        room.push_back((uint32_t)std::stoul(line.substr(a + 1, b - a - 1)));
+        std::vector<uint8_t> f = unhex(line.substr(b + 1));
+        // headroom 32 as the reference's BufferPool allocates (buffer_pool.hpp:57)
+        bufs.emplace_back(new netflow_amd::PacketBuffer(room.back() + 32, 32, f.size()));
+        std::memset(bufs.back()->raw_data_ptr_, 0, room.back() + 32);
+        if (!f.empty()) std::memcpy(bufs.back()->get_data_start_ptr(), f.data(), f.size());
+        pkts.emplace_back(new netflow_amd::Packet(bufs.back().get()));
+    }
+    const size_t n = pkts.size();
+    std::vector<netflow_amd::Packet*> raw;
+    for (auto& p : pkts) raw.push_back(p.get());
+    std::unique_ptr<bool[]> ok(new bool[n ? n : 1]);
+    std::vector<uint8_t> st(n, 0xEE);
+    if (!single) {
+        int rc = netflow_amd::vlan_batch(raw.data(), ops.data(), n, ok.get(), st.data());
+        if (rc) { std::fprintf(stderr, "rc=%d\n", rc); return 2; }
+    } else {
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t kind = ops[i] & NFCS_VLAN_OP_MASK;
+            ok[i] = kind == NFCS_VLAN_PUSH ? raw[i]->push_vlan(ops[i] & 0xFFF, (ops[i] >> 13) & 7)
+                  : kind == NFCS_VLAN_POP ? raw[i]->pop_vlan() : false;
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        auto* b = raw[i]->get_buffer();
+        std::printf("%d %d %zu %s\n", ok[i] ? 1 : 0, (int)st[i], b->get_data_length(),
+                    hex(b->get_data_start_ptr(), room[i]).c_str());
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (mode == "cpu") return cpu_checks();
+    if (mode == "vlan" || mode == "vlan1") return vlan_mode(mode == "vlan1");
     std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
     std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
     std::string line;

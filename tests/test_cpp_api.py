@@ -57,3 +57,32 @@ def test_cpp_update_matches_oracle(exe, mode):
         assert hx == exp.hex()
         if mode == "batch":
             assert int(st) == est
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["vlan", "vlan1"])
+def test_cpp_vlan_matches_reference_behaviour(exe, mode):
+    """netflow_amd::vlan_batch and Packet::push_vlan / pop_vlan against the oracle (pinned to
+    the reference by tests/golden/kat_vlan.json / vlan_ref.npz): new bytes, length and return."""
+    import numpy as np
+    from vlan_common import random_vlan_case
+    frames, ops, caps = random_vlan_case(77, 3000 if mode == "vlan" else 150)
+    room = [int(c) for c in caps]  # the buffer's bytes from the data start = the push capacity
+    inp = "\n".join(f"{int(o)} {r} {f.hex()}" for o, r, f in zip(ops, room, frames)) + "\n"
+    r = subprocess.run([exe, mode], input=inp, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(frames)
+    for i, (f, line) in enumerate(zip(frames, lines)):
+        okv, st, nlen, hx = line.split(" ")
+        buf = np.zeros(max(room[i], oracle.vlan_window(len(f))), dtype=np.uint8)
+        buf[:len(f)] = np.frombuffer(f, dtype=np.uint8)
+        ln = np.array([len(f)], dtype=np.uint32)
+        est = oracle.lib().nfo_vlan(oracle._ptr(buf), oracle._ptr(ln, oracle._u32p), room[i], int(ops[i]))
+        if (est & 0x1F) == 14:
+            continue
+        assert int(okv) == (1 if est & 0x20 else 0), i
+        assert int(nlen) == int(ln[0]), i
+        assert hx == buf[:room[i]].tobytes().hex(), i
+        if mode == "vlan":
+            assert int(st) == est, i
