@@ -134,14 +134,20 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                 nfcs_patch* d_patch, void* stream);
 
-/* Same on host memory (NIC / socket buffers). Frames are staged through the context's
- * pinned ring in chunks (H2D copy, kernel, D2H copy overlapped on two streams) and the
- * updated bytes are written back into h_arena. Synchronous. h_arena need not be pinned;
- * pinned memory (nfcs_host_alloc) avoids one host-side copy. Descriptors must be sorted by
- * off16 (frames in arena order, as a NIC ring or nfcs_layout_config lays them out).
- * flags: NFCS_HOST_PATCH_ONLY copies back 8-byte nfcs_patch records instead of whole
- * frames and applies them on the host. */
+/* Same on host memory (NIC / socket buffers). Synchronous. Descriptors must be sorted by
+ * off16 (frames in arena order, as a NIC ring or nfcs_layout_config lays them out). Frames go
+ * H2D in chunks on two streams (from a pageable arena through the context's pinned ring, copied
+ * by host threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs
+ * per chunk, and only the 8-byte nfcs_patch records come back and are applied on the host.
+ * flags:
+ *   NFCS_HOST_FRAMES     copy whole frames back instead of patch records (same bytes, slower)
+ *   NFCS_HOST_ZERO_COPY  pinned arenas only: the kernel reads the frames over PCIe in place and
+ *                        writes the checksum bytes straight back (no staging copies)
+ *   NFCS_HOST_PATCH_ONLY the default since ABI 1 session 2; accepted and ignored
+ * Rates: DESIGN.md §7. */
 #define NFCS_HOST_PATCH_ONLY 1u
+#define NFCS_HOST_ZERO_COPY 2u
+#define NFCS_HOST_FRAMES 4u
 NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
                               const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
                               uint32_t flags);

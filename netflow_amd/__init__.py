@@ -45,7 +45,7 @@ FLOW_KEY_DTYPE = np.dtype([("hash", "<u4"), ("vlan_id", "<u2"), ("ethertype", "<
                            ("reserved", "u1", (6,)), ("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,))])
 assert FLOW_KEY_DTYPE.itemsize == 64
 CFG_C0, CFG_C1, CFG_C2, CFG_C3 = 0, 1, 2, 3
-HOST_PATCH_ONLY = 1
+HOST_PATCH_ONLY, HOST_ZERO_COPY, HOST_FRAMES = 1, 2, 4
 PATCH_NONE = 0xFFFF
 
 
@@ -207,6 +207,12 @@ class Engine:
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
 
+    def host_array(self, nbytes: int) -> np.ndarray:
+        """A pinned host uint8 array (nfcs_host_alloc), freed with the engine's context."""
+        p = _vp()
+        _check(lib().nfcs_host_alloc(self.ctx, max(int(nbytes), 16), ctypes.byref(p)), "host_alloc")
+        return np.ctypeslib.as_array((ctypes.c_uint8 * max(int(nbytes), 16)).from_address(p.value))[:nbytes]
+
     def sync(self, stream=None):
         _check(lib().nfcs_stream_sync(self.ctx, stream), "stream_sync")
 
@@ -219,8 +225,11 @@ class Engine:
                                         ptr(status), ptr(patch), stream), "nfcs_update_device")
 
     def update_host(self, arena: np.ndarray, desc: np.ndarray, want_status: bool = True,
-                    patch_only: bool = False) -> np.ndarray | None:
-        """Batched update_checksums() on host frames (in place); returns status bytes."""
+                    mode: str = "patch") -> np.ndarray | None:
+        """Batched update_checksums() on host frames (in place); returns status bytes.
+        mode: "patch" (default: frames H2D, patch records back), "frames" (whole frames back),
+        "zero_copy" (pinned arena from host_array(): the kernel reads it over PCIe in place)."""
+        flags = {"patch": 0, "frames": HOST_FRAMES, "zero_copy": HOST_ZERO_COPY}[mode]
         assert arena.dtype == np.uint8 and arena.flags.c_contiguous
         desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
         n = len(desc)
@@ -228,7 +237,7 @@ class Engine:
         _check(lib().nfcs_update_host(self.ctx, arena.ctypes.data, arena.nbytes,
                                       desc.ctypes.data if n else None, n,
                                       status.ctypes.data if want_status and n else None,
-                                      HOST_PATCH_ONLY if patch_only else 0), "nfcs_update_host")
+                                      flags), "nfcs_update_host")
         return status
 
     def l3_forward_device(self, arena, arena_bytes: int, desc, nh, n: int, table, table_n: int,

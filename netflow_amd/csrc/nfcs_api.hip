@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "nfcs_internal.h"
 
@@ -22,6 +24,7 @@ struct nfcs_ctx {
     hipEvent_t done[kSlots] = {nullptr, nullptr};
     size_t stage_bytes = 0;   // arena bytes per slot
     uint32_t stage_pkts = 0;  // descriptors per slot
+    int copy_threads = 8;     // host threads for pageable <-> pinned staging copies
     uint8_t* d_arena[kSlots] = {nullptr, nullptr};
     nfcs_desc* d_desc[kSlots] = {nullptr, nullptr};
     uint8_t* d_status[kSlots] = {nullptr, nullptr};
@@ -83,8 +86,29 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
+// memcpy split across threads: one host thread copies pageable memory at ~15-25 GB/s, below
+// what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned).
+void par_memcpy(void* dst, const void* src, size_t bytes, int threads) {
+    const size_t kMin = 4u << 20;
+    if (threads <= 1 || bytes < 2 * kMin) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t t = std::min<size_t>((size_t)threads, bytes / kMin);
+    const size_t per = (bytes / t + 4095) & ~size_t(4095);
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < t; ++i) {
+        const size_t o = i * per;
+        if (o >= bytes) break;
+        th.emplace_back([=] { memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o)); });
+    }
+    memcpy(dst, src, std::min(per, bytes));
+    for (auto& x : th) x.join();
+}
+
 int ensure_host_pipeline(nfcs_ctx* ctx) {
     if (ctx->d_arena[0]) return NFCS_OK;
+    ctx->copy_threads = env_int("NFCS_COPY_THREADS", 8);
     ctx->stage_bytes = (size_t)env_int("NFCS_STAGE_MB", 64) << 20;
     ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
@@ -111,6 +135,50 @@ bool is_pinned(const void* p) {
         return false;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+// Pinned host arena: the kernel reads the frames over PCIe where they are and writes the 2+2
+// checksum bytes straight back (host memory from hipHostMalloc is mapped into the GPU's address
+// space). Only descriptors (8 B/packet) go H2D and statuses (1 B/packet) D2H, in chunks on the
+// two pipeline streams; frames cross the link once, in one direction.
+int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
+                          const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status) {
+    void* dptr = nullptr;
+    NFCS_HIP(hipHostGetDevicePointer(&dptr, h_arena, 0));
+    uint8_t* d_arena = static_cast<uint8_t*>(dptr);
+    uint32_t cnt[nfcs_ctx::kSlots] = {0, 0}, first[nfcs_ctx::kSlots] = {0, 0};
+    auto finish = [&](int s) -> int {
+        if (!cnt[s]) return NFCS_OK;
+        NFCS_HIP(hipEventSynchronize(c->done[s]));
+        if (h_status) memcpy(h_status + first[s], c->h_status[s], cnt[s]);
+        cnt[s] = 0;
+        return NFCS_OK;
+    };
+    int s = 0;
+    for (uint32_t i = 0; i < n; s ^= 1) {
+        int rc = finish(s);
+        if (rc) return rc;
+        const uint32_t m = std::min<uint32_t>(n - i, c->stage_pkts);
+        hipStream_t st = c->hs[s];
+        memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        NFCS_HIP(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
+                                hipMemcpyHostToDevice, st));
+        NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, c->d_desc[s], m, 0u,
+                                     h_status ? c->d_status[s] : nullptr, nullptr, st,
+                                     // fused kernel: a separate patch pass buys nothing
+                                     // when the stores go over PCIe anyway
+                                     (c->variant == 0 || c->variant == 8) ? 24 : c->variant,
+                                     c->grid, nfcs::Work{}));
+        if (h_status)
+            NFCS_HIP(hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st));
+        NFCS_HIP(hipEventRecord(c->done[s], st));
+        first[s] = i;
+        cnt[s] = m;
+        i += m;
+    }
+    int rc = finish(s);
+    if (rc) return rc;
+    return finish(s ^ 1);
 }
 
 }  // namespace
@@ -251,8 +319,14 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         if (h_desc[i].off16 < h_desc[i - 1].off16) return NFCS_EINVAL;  // must be arena order
     int rc = ensure_host_pipeline(c);
     if (rc) return rc;
-    const bool patch_only = flags & NFCS_HOST_PATCH_ONLY;
+    // default: frames H2D, 8-byte patch records D2H, applied here (measured fastest); whole
+    // frames back only on request (NFCS_HOST_FRAMES)
+    const bool patch_only = !(flags & NFCS_HOST_FRAMES);
     const bool pinned = is_pinned(h_arena);
+    if (flags & NFCS_HOST_ZERO_COPY) {
+        if (!pinned) return NFCS_EINVAL;
+        return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status);
+    }
 
     struct Chunk { uint32_t i0, i1; uint64_t base, bytes; bool used; };
     Chunk slot[nfcs_ctx::kSlots] = {};
@@ -273,7 +347,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                 if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
             }
         } else if (!pinned) {
-            memcpy(h_arena + k.base, c->h_arena[s], k.bytes);
+            par_memcpy(h_arena + k.base, c->h_arena[s], k.bytes, c->copy_threads);
         }
         if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
         k.used = false;
@@ -306,7 +380,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint32_t m = i1 - i;
         const uint8_t* src = h_arena + base;
         if (!pinned) {
-            memcpy(c->h_arena[s], src, k.bytes);
+            par_memcpy(c->h_arena[s], src, k.bytes, c->copy_threads);
             src = c->h_arena[s];
         }
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));

@@ -186,14 +186,14 @@ def test_bad_descriptors_and_empty_batch(engine):
     engine.sync()
 
 
-@pytest.mark.parametrize("patch_only", [False, True])
-def test_host_path_pipeline(engine, patch_only):
+@pytest.mark.parametrize("mode", ["patch", "frames"])
+def test_host_path_pipeline(engine, mode):
     """nfcs_update_host: frames in pageable host memory, chunked through the pinned ring."""
     frames = oracle.fuzz_frames(11, 0, 40000)
     arena, desc = oracle.pack_frames(frames)
     ref = arena.copy()
     rst, _ = oracle.update_batch(ref, desc, nthreads=8)
-    st = engine.update_host(arena, desc, patch_only=patch_only)
+    st = engine.update_host(arena, desc, mode=mode)
     assert np.array_equal(st, rst)
     assert np.array_equal(arena, ref)
 
@@ -204,3 +204,19 @@ def test_host_path_config_multi_chunk(engine):
     rst, _ = oracle.update_batch(ref, desc, nthreads=8)
     st = engine.update_host(arena, desc)
     assert np.array_equal(st, rst) and np.array_equal(arena, ref)
+
+
+@pytest.mark.parametrize("mode", ["zero_copy", "patch", "frames"])
+def test_host_path_pinned(engine, mode):
+    """nfcs_update_host on a pinned arena: zero-copy (the kernel reads the frames over PCIe in
+    place and writes the checksum bytes back) or staged through the ring; fuzz frames incl. jumbo
+    and out-of-arena descriptors."""
+    frames = oracle.fuzz_frames(12, 0, 30000)
+    packed, desc = oracle.pack_frames(frames)
+    arena = engine.host_array(packed.nbytes)
+    arena[:] = packed
+    ref = packed.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    st = engine.update_host(arena, desc, mode=mode)
+    assert np.array_equal(st, rst)
+    assert np.array_equal(arena, ref)

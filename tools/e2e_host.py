@@ -5,7 +5,9 @@ Frames start and end in host memory (NIC/socket buffers): the engine stages them
 pinned ring (H2D copy, kernel, D2H copy, overlapped on two streams). Measures, for config C1:
   * pageable host arena, whole frames copied back;
   * pageable host arena, only 8-byte patch records copied back and applied on the host;
-  * pinned host arena (nfcs_host_alloc), whole frames copied back.
+  * pinned host arena (nfcs_host_alloc), staged, whole frames / patch records copied back;
+  * pinned host arena, zero-copy (the kernel reads the frames over PCIe in place).
+Every mode's result must equal the reference's (C1 digest, tests/golden/configs.json).
 Prints one JSON object per mode (GB/s of frame bytes, host wall clock).
 """
 import ctypes
@@ -21,30 +23,40 @@ sys.path.insert(0, ROOT)
 import netflow_amd as nf  # noqa: E402
 
 
+def result_digest(eng, arena, d_desc, n):
+    """Order-independent digest of the updated frames (nfcs_digest_device on a device copy),
+    compared with the reference's C1 digest (tests/golden/configs.json)."""
+    d = eng.alloc(arena.nbytes).upload(arena)
+    g = eng.digest_device(d, arena.nbytes, d_desc, n, 0)
+    d.free()
+    return g
+
+
 def main(n=1 << 20, reps=5):
     eng = nf.Engine(0)
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(1, 20250620, 0, n)
     src = d_arena.download(np.uint8, nbytes)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     out = []
-    for mode in ("pageable_frames", "pageable_patch", "pinned_frames"):
-        if mode.startswith("pinned"):
-            p = ctypes.c_void_p()
-            nf._check(nf.lib().nfcs_host_alloc(eng.ctx, nbytes, ctypes.byref(p)), "host_alloc")
-            arena = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
-        else:
-            arena = np.empty(nbytes, dtype=np.uint8)
+    want = int(json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+               ["configs"]["1"]["digest_out"], 16)
+    pinned = eng.host_array(nbytes)
+    for mode in ("pageable_frames", "pageable_patch", "pinned_frames", "pinned_patch", "pinned_zero_copy"):
+        arena = pinned if mode.startswith("pinned") else np.empty(nbytes, dtype=np.uint8)
+        kw = dict(want_status=False, mode=mode.split("_", 1)[1])
         arena[:] = src
-        eng.update_host(arena, hdesc, want_status=False, patch_only=mode.endswith("patch"))  # warm
+        eng.update_host(arena, hdesc, **kw)  # warm
+        assert result_digest(eng, arena, d_desc, n) == want, mode
         ts = []
         for _ in range(reps):
             arena[:] = src
             t0 = time.perf_counter()
-            eng.update_host(arena, hdesc, want_status=False, patch_only=mode.endswith("patch"))
+            eng.update_host(arena, hdesc, **kw)
             ts.append(time.perf_counter() - t0)
+        assert result_digest(eng, arena, d_desc, n) == want, mode
         t = min(ts)
         r = {"mode": mode, "packets": n, "frame_bytes": frame_bytes, "seconds": t,
-             "GBps": frame_bytes / t / 1e9}
+             "GBps": frame_bytes / t / 1e9, "digest": f"{want:016x}"}
         print(json.dumps(r), flush=True)
         out.append(r)
     return out
