@@ -46,7 +46,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 // arena footprint per packet is at least kSplitMeanBytes.
 constexpr uint64_t kSplitMeanBytes = 2048;
 inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
-    return variant == 8 || variant == 22 || variant == 23 ||
+    return variant == 8 || variant == 22 || variant == 23 ||  // 22/23: experiments build only
            (variant == 0 && n > 0 && arena_bytes / n >= kSplitMeanBytes);
 }
 // variants that stage patch records in a context workspace (split mode)

@@ -824,6 +824,7 @@ __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restri
     }
 }
 
+#ifdef NFCS_EXPERIMENTS  // measured alternatives, measurement builds only
 // =============================================================================================
 // v4: lane-per-packet planning, row-per-packet summing.
 //
@@ -1116,6 +1117,302 @@ __global__ __launch_bounds__(kBlock, 1) void update_lp_kernel(uint8_t* __restric
     }
 }
 
+template <int K, int R, int P, int DBG, int KW>
+__global__ __launch_bounds__(kBlock, 1) void update_win_kernel(uint8_t* __restrict__ arena,
+                                                              uint64_t arena_bytes,
+                                                              const nfcs_desc* __restrict__ desc,
+                                                              uint32_t n, uint32_t base16,
+                                                              uint8_t* __restrict__ status,
+                                                              nfcs_patch* __restrict__ patch) {
+    static_assert(P == 64, "one plan lane per packet");
+    __shared__ LpShared<P> sh;
+    constexpr uint32_t MAXT = 6144;  // chunks of one wave's window: one map byte each
+    __shared__ __attribute__((aligned(16))) uint8_t wmap[kWavesPerBlock][MAXT];
+    __shared__ uint32_t wsums[kWavesPerBlock][P];
+    uint32_t w_start = 0, w_nre = 0, w_live = 0, w_ok = 1;  // this lane's packet, for the window
+    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
+    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * P;
+    if (pw >= n) return;
+    // ---- phase A: lane `lane` plans packet pw + lane -----------------------------------------
+    {
+        const uint64_t p = pw + lane;
+        const bool valid = p < n;
+        const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
+        const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
+        const bool bad = valid && ((d.off16 < base16) ||
+                                   (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
+        const bool live = valid && !bad;
+        const uint32_t len = live ? d.len : 0u;
+        uint8_t* frame = arena + (live ? off : 0);
+        const uint32_t nch = (len + 15u) >> 4;
+        uint32_t h[20];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint4 c = ld16<0>(((uint32_t)k < nch) ? (const uint4*)frame + k : &g_zero16);
+            h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
+        }
+        RPlan Q = lane_plan(h, len);
+        uint32_t l4w = NFCS_PATCH_NONE, done = 0;
+        if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
+            Q = slow_plan(frame, len);
+            if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
+                const SeqOut o = seq_update(frame, len);
+                Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
+                Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
+                l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
+                done = RF_DONE;
+            }
+        }
+        if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
+        const uint32_t re = (Q.flags & F_L4) ? Q.re : 0u;
+        // phase B sums whole chunks from chunk 0: the frame dwords below lo4 = rs & ~3 (all in
+        // h: rs <= l2 + 60 < 80) are subtracted here once, so no chunk needs a start mask
+        {
+            const uint32_t lo4 = Q.rs & ~3u;
+            uint32_t hs = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 20; ++q) hs = wsum((4u * q < lo4) ? h[q] : 0u, hs);
+            if (re) Q.corr -= hs;
+        }
+        const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
+        uint4* r = sh.rec[wv][lane];
+        r[0] = make_uint4(live ? (uint32_t)(off >> 4) : 0u, re | (Q.flags << 24) | (valid ? RF_LIVE : 0u) | done,
+                          (Q.rs & 0xFFFFu) | (Q.fs << 16), Q.corr);
+        r[1] = make_uint4(ipw, Q.st, l4w, 0u);
+        w_start = live ? (uint32_t)(off >> 4) : 0u;
+        w_nre = (re + 15u) >> 4;
+        w_live = live;
+        w_ok = !bad;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // ---- window mode: the wave's packets lie in arena order without gaps bigger than their
+    // regions: stream [W0, W0 + T) flat (chunk W0 + g in lane g % 64 of slot g / 64 — every
+    // lane's load useful, short frames or long), each chunk finds its packet in an LDS map
+    {
+        const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
+        const bool has = w_live && w_nre != 0;
+        const uint64_t hb = __builtin_amdgcn_ballot_w64(has);
+        bool ok = __builtin_amdgcn_ballot_w64(!w_ok) == 0 && hb != 0;
+        uint32_t W0 = 0, T = 0;
+        if (ok) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(hb), last = 63u - (uint32_t)__builtin_clzll(hb);
+            W0 = (uint32_t)__builtin_amdgcn_readlane((int)w_start, (int)first);
+            T = (uint32_t)__builtin_amdgcn_readlane((int)(w_start + w_nre), (int)last) - W0;
+            // region lanes in ascending order: the previous region lanes' ends <= my start
+            uint32_t x = has ? (w_start + w_nre - W0) : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {  // inclusive running max over lanes
+                const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane >= (uint32_t)d) ? lane - d : lane) * 4u), (int)x);
+                x = (lane >= (uint32_t)d) ? max(x, y) : x;
+            }
+            uint32_t prev_end = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1u : 0u) * 4u), (int)x);
+            if (lane == 0) prev_end = 0;
+            const bool bad_order = has && (w_start < W0 || w_start - W0 < prev_end);
+            uint32_t dense = has ? w_nre : 0u;  // region chunks of the wave
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) dense += (uint32_t)__shfl_xor((int)dense, d);
+            ok = __builtin_amdgcn_ballot_w64(bad_order) == 0 && T <= MAXT && T <= 2u * dense + 64u;
+        }
+        if (ok) {
+            uint8_t* map = wmap[wv];
+            // map[g] = 0xFF (no region), j, or j | 0x40 on a region's last chunk
+            for (uint32_t q = lane; q < (T + 15u) >> 4; q += 64u)
+                ((uint4*)map)[q] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+            wsums[wv][lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            if (has) {
+                const uint32_t a = w_start - W0, b = a + w_nre;  // map bytes [a, b)
+                const uint32_t jb = lane * 0x01010101u;
+                uint32_t c = a;
+                for (; c < b && (c & 3u); ++c) map[c] = (uint8_t)lane;
+                for (; c + 4 <= b; c += 4) *(uint32_t*)(map + c) = jb;
+                for (; c < b; ++c) map[c] = (uint8_t)lane;
+                map[b - 1] = (uint8_t)(lane | 0x40u);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const uint4* src = (const uint4*)arena + W0;
+            for (uint32_t g0 = 0; g0 < T; g0 += 64u * KW) {
+                uint4 v[KW];
+                uint32_t m[KW];
+#pragma unroll
+                for (int k = 0; k < KW; ++k) {
+                    const uint32_t g = g0 + 64u * k + lane;
+                    v[k] = ld16<1>((g < T) ? src + g : &g_zero16);
+                    m[k] = (g < T) ? map[g] : 0xFFu;
+                }
+#pragma unroll
+                for (int k = 0; k < KW; ++k) {
+                    if (m[k] != 0xFFu) {
+                        const uint32_t j = m[k] & 63u;
+                        uint32_t a = add_chunk(v[k], 0u);
+                        if (m[k] & 0x40u) {  // the region's last chunk: bytes past re, odd tail
+                            const uint4 r0 = sh.rec[wv][j][0];
+                            const uint32_t re = r0.y & 0x1FFFFu, o = (re - 1u) & ~15u;
+                            uint32_t ex = 0;
+#pragma unroll
+                            for (uint32_t jj = 0; jj < 4; ++jj) {
+                                const int nb = (int)re - (int)(o + 4u * jj);
+                                const uint32_t mk = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
+                                ex = wsum(comp(v[k], jj) & mk, ex);
+                            }
+                            a -= ex;
+                            const uint32_t t = re - 1u;
+                            if ((r0.y >> 24) & F_TAIL)
+                                a += 255u * ((comp(v[k], (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+                        }
+                        atomicAdd(&wsums[wv][j], a);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // lane j: fold, write back, status / patch
+            if (lane < cnt) {
+                const uint4 r0 = sh.rec[wv][lane][0], r1 = sh.rec[wv][lane][1];
+                const uint32_t fl = (r0.y >> 24) & 0x1Fu, fs = r0.z >> 16;
+                const bool done = r0.y & RF_DONE, live = r0.y & RF_LIVE;
+                uint32_t l4w = r1.z;
+                if (!done && (fl & F_L4)) {
+                    uint32_t c = (~fold32(wsums[wv][lane] + r0.w)) & 0xFFFFu;
+                    if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
+                    l4w = fs | (c << 16);
+                }
+                const uint32_t ipw = r1.x;
+                uint8_t* frame = arena + (uint64_t)r0.x * 16u;
+                if (!(DBG & 1) && live && !done) {
+                    if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) {
+                        frame[ipw & 0xFFFFu] = (uint8_t)(ipw >> 16);
+                        frame[(ipw & 0xFFFFu) + 1] = (uint8_t)(ipw >> 24);
+                    }
+                    if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) {
+                        frame[l4w & 0xFFFFu] = (uint8_t)(l4w >> 16);
+                        frame[(l4w & 0xFFFFu) + 1] = (uint8_t)(l4w >> 24);
+                    }
+                }
+                if (live) {
+                    const uint64_t p = pw + lane;
+                    if (status) status[p] = (uint8_t)r1.y;
+                    if (patch) {
+                        uint2 pr;
+                        pr.x = (ipw & 0xFFFFu) | (l4w << 16);
+                        pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
+                        ((uint2*)patch)[p] = pr;
+                    }
+                }
+            }
+            return;
+        }
+    }
+    // ---- phase B: rows of R lanes sum their packet's region --------------------------------
+    constexpr uint32_t PR = 64 / R;  // packets per wave instruction
+    const uint32_t rl = lane & (R - 1), row = lane / R;
+    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
+    const uint32_t iters = (cnt + PR - 1) / PR;
+
+    struct Stage {
+        uint4 v[K];
+        uint4 t;   // the region's last chunk (end excess, odd-tail byte)
+        uint4 r0;  // off16, re | flags, rs | fs, corr (header prefix folded in)
+        uint32_t idx;
+    };
+    auto stage = [&](Stage& S, uint32_t it) {
+        // rlv is opaque in every iteration, so per-slot offsets are recomputed rather than
+        // hoisted out of the loop into long-lived VGPRs
+        uint32_t rlv = rl;
+        asm volatile("" : "+v"(rlv));
+        S.idx = it * PR + row;
+        S.r0 = sh.rec[wv][S.idx][0];
+        const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
+        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
+        // chunks 0 .. nre-1 in full (chunks past the region read zeros)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rlv + (uint32_t)R * k;
+            const uint4* a = (c < nre) ? src + c : &g_zero16;
+            S.v[k] = (k == 0) ? ld16<0>(a) : ld16<1>(a);
+        }
+        S.t = ld16<0>(nre ? src + (nre - 1u) : &g_zero16);
+    };
+    auto finish = [&](const Stage& S) {
+        uint32_t rlv = rl;
+        asm volatile("" : "+v"(rlv));
+        const uint32_t fl = (S.r0.y >> 24) & 0x1Fu;
+        const uint32_t re = S.r0.y & 0x1FFFFu, fs = S.r0.z >> 16;
+        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = add_chunk(S.v[k], acc);
+        const uint32_t nre = (re + 15u) >> 4;
+        const uint32_t cmax = wave_max_rows<R>(nre);
+        // jumbo frames: the rest in batches of K2 slots (the next stage's K slots are in flight,
+        // so a K-slot batch here would cost 30 VGPRs for the whole kernel)
+        constexpr int K2 = 2;
+        for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K2) {
+            uint4 w[K2];
+#pragma unroll
+            for (int k = 0; k < K2; ++k) {
+                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
+            }
+#pragma unroll
+            for (int k = 0; k < K2; ++k) acc = add_chunk(w[k], acc);
+        }
+        if (rl == 0 && re) {  // the last chunk's bytes past re; the odd trailing byte (903-905)
+            const uint32_t o = (re - 1u) & ~15u;
+            uint32_t ex = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int nb = (int)re - (int)(o + 4u * j);
+                const uint32_t m = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
+                ex = wsum(comp(S.t, j) & m, ex);
+            }
+            acc -= ex;
+            const uint32_t t = re - 1u;
+            if (fl & F_TAIL) acc += 255u * ((comp(S.t, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+        }
+        const uint32_t z = row_sum<R>(acc) + S.r0.w;
+        const uint4 r1 = sh.rec[wv][S.idx][1];
+        const bool done = S.r0.y & RF_DONE, live = S.r0.y & RF_LIVE;
+        uint32_t l4w = r1.z;
+        if (!done && (fl & F_L4)) {
+            uint32_t c = (~fold32(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
+            if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
+            l4w = fs | (c << 16);
+        }
+        const uint32_t ipw = r1.x;
+        uint8_t* frame = arena + (uint64_t)S.r0.x * 16u;
+        if (!(DBG & 1) && live && !done && rl < 4) {
+            const uint32_t w = (rl & 2u) ? l4w : ipw;
+            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+        }
+        if (live && rl == 0) {
+            const uint64_t p = pw + S.idx;
+            if (status) status[p] = (uint8_t)r1.y;
+            if (patch) {
+                uint2 pr;
+                pr.x = (ipw & 0xFFFFu) | (l4w << 16);
+                pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
+                ((uint2*)patch)[p] = pr;
+            }
+        }
+    };
+    Stage A, B;
+    stage(A, 0);
+    for (uint32_t it = 0; it < iters; it += 2) {
+        if (it + 1 < iters) stage(B, it + 1);
+        finish(A);
+        if (it + 1 >= iters) break;
+        if (it + 2 < iters) stage(A, it + 2);
+        finish(B);
+    }
+}
+
+#endif  // NFCS_EXPERIMENTS
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, hipStream_t stream, int variant, int grid,
@@ -1156,6 +1453,25 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 26: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
                                 dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // 8-lane rows K=12, branch-free sums
+    case 8: {  // split: checksum pass without frame stores, then the patch pass
+        nfcs_patch* pp = patch ? patch : ws;
+        if (!pp) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
+                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
+                           nofwd);
+        int ga = (int)((n + kBlock - 1) / kBlock);
+        if (ga > di.cus * 8) ga = di.cus * 8;
+        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+                           base16, pp);
+        break;
+    }
+#ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+    case 40: hipLaunchKernelGGL((update_win_kernel<6, 16, 64, 0, 6>), dim3((n + 255u) / 256u),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch); break;  // window mode (flat stream per wave), K=6
+    case 41: hipLaunchKernelGGL((update_win_kernel<6, 16, 64, 0, 8>), dim3((n + 255u) / 256u),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch); break;  // window mode, 8 slots per flat step
     case 20: NFCS_LP(6, 16, 0, patch); break;  // v4: lane plans, 16-lane row sums
     case 21: NFCS_LP(6, 8, 0, patch); break;   // v4: lane plans, 8-lane row sums
     case 22:
@@ -1170,19 +1486,6 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                            base16, pp);
         break;
     }
-    case 8: {  // split: checksum pass without frame stores, then the patch pass
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
-                           nofwd);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
-    }
-#ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
     case 101: NFCS_ROWSP(6, 2, 16, 1, patch); break;  // no frame stores
     case 102: NFCS_ROWSP(6, 2, 16, 2, patch); break;  // no parse (fixed C1 plan)
     case 103: NFCS_ROWSP(6, 2, 16, 3, patch); break;  // neither
