@@ -39,6 +39,9 @@ import netflow_amd as nf  # noqa: E402
 
 SEED = 20250620
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip parameters)
+# measured on the MI355X box (tools/stream_read.hip, tools/stream_rw.hip; profiles/r01_stream_microbench.md):
+STREAM_READ_GBPS = 7007.0  # best read-only stream (nt loads)
+STREAM_RW_GBPS = 4839.0    # best read stream with one in-place store per 1536-byte frame
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 C4_PACKETS_PER_GPU = 1 << 22
 WORKLOAD = {
@@ -416,6 +419,19 @@ def main():
                      "algorithmic_bytes_per_launch": int(algo_bytes)},
         "parity": {"digest": got, "reference_digest": want, "match": parity_ok, "all_ranks": parity_all},
     }
+    if args.op == "update":
+        # frame-only and checksummed-only (frame minus its 14-byte L2 header;
+        # the synthetic frames are untagged) rates, and the fraction of the read-only stream
+        # ceiling measured on the same MI355X (profiles/r01_stream_microbench.md)
+        t_step = wall / args.steps
+        csum_bytes = D.sum(frame_bytes - 14.0 * n)
+        out["bytes"] = {"frame_GBps": round(total_frame_bytes / t_step / 1e9, 2),
+                        "checksummed_GBps": round(csum_bytes / t_step / 1e9, 2),
+                        "algorithmic_GBps_kernel": round(achieved, 1)}
+        out["stream_ceiling"] = {"read_only_GBps": STREAM_READ_GBPS,
+                                 "frac_of_read_only": round(achieved / STREAM_READ_GBPS, 4),
+                                 "read_plus_one_store_per_frame_GBps": STREAM_RW_GBPS,
+                                 "source": "profiles/r01_stream_microbench.md"}
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
