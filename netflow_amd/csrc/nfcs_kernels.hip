@@ -1411,6 +1411,182 @@ __global__ __launch_bounds__(kBlock, 1) void update_win_kernel(uint8_t* __restri
     }
 }
 
+
+// ---- flat-M: M packets per wave laid back to back over 64 lanes x K slots ---------------------
+// A wave owns M consecutive packets (M from the batch's mean footprint, host-chosen). Flat
+// chunk g of the wave is chunk g - pre[j] of packet j, pre = exclusive prefix of the packets'
+// chunk counts: every lane's load is useful whatever the frame lengths, and all of them are
+// issued at wave start (no loop). The chunks are summed as soon as they land — whole frames,
+// bytes >= len masked — into an LDS sum per packet, so the chunk registers die before any
+// planning; the lanes holding a frame's first 80 bytes drop them into an LDS header buffer and
+// the lane holding its last chunk its last byte. Lane j then plans packet j from LDS
+// (lane_plan) and removes what lies outside the L4 region [rs, re) exactly: the frame dwords
+// below rs & ~3 from the header buffer, the bytes past re (rare: frames longer than their L4
+// length) from memory.
+DEV uint32_t sum_bytes_le(const uint8_t* f, uint32_t a, uint32_t b) {  // LE-word sum of [a, b)
+    uint32_t s = 0;
+    for (uint32_t o = a; o < b; ++o) s += (uint32_t)f[o] << ((o & 1u) ? 8 : 0);
+    return s;
+}
+
+template <int K, int M, int DBG>
+__global__ __launch_bounds__(kBlock, 1) void update_flat_kernel(uint8_t* __restrict__ arena,
+                                                                uint64_t arena_bytes,
+                                                                const nfcs_desc* __restrict__ desc,
+                                                                uint32_t n, uint32_t base16,
+                                                                uint8_t* __restrict__ status,
+                                                                nfcs_patch* __restrict__ patch) {
+    static_assert(M >= 1 && M <= 16, "packets per wave");
+    __shared__ uint32_t fsum[kWavesPerBlock][16];
+    __shared__ uint32_t ftail[kWavesPerBlock][16];
+    __shared__ uint4 fhdr[kWavesPerBlock][16][5];
+    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
+    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * M;
+    if (pw >= n) return;
+    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)M ? (n - pw) : (uint64_t)M);
+    const bool valid = lane < cnt;
+    const uint64_t p = pw + lane;
+    const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
+    const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
+    const bool bad = valid && ((d.off16 < base16) ||
+                               (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
+    const bool live = valid && !bad;
+    const uint32_t len = live ? d.len : 0u;
+    uint8_t* frame = arena + (live ? off : 0);
+    const uint32_t nch = (len + 15u) >> 4;
+    // exclusive prefix of the chunk counts, frame bases and lengths, as wave-uniform values
+    uint32_t P[M], Ln[M];
+    uint64_t F[M];
+    uint32_t T = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        P[i] = T;
+        Ln[i] = (uint32_t)__builtin_amdgcn_readlane((int)len, i);
+        T += (Ln[i] + 15u) >> 4;
+        F[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)frame >> 32), i) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)frame, i);
+    }
+    if (lane < 16) {
+        fsum[wv][lane] = 0;
+        ftail[wv][lane] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // flat batches of K slots: slot k, lane l -> flat chunk g = cb + 64k + l
+    for (uint32_t cb = 0; cb < T; cb += 64u * K) {
+        uint4 v[K];
+        uint32_t cj[K];  // c | j << 16, 0xFFFF0000 past T
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t g = cb + 64u * k + lane;
+            uint32_t j = 0, pre = 0;
+            uint64_t base = F[0];
+#pragma unroll
+            for (int i = 1; i < M; ++i) {
+                const bool ge = g >= P[i];
+                j = ge ? (uint32_t)i : j;
+                pre = ge ? P[i] : pre;
+                base = ge ? F[i] : base;
+            }
+            const bool in = g < T;
+            v[k] = ld16<1>(in ? (const uint4*)base + (g - pre) : &g_zero16);
+            cj[k] = in ? ((g - pre) | (j << 16)) : 0xFFFF0000u;
+        }
+        const uint32_t rl = lane & 15u;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t j = cj[k] >> 16, c = cj[k] & 0xFFFFu;
+            uint32_t a = 0;
+            if (j != 0xFFFFu) {
+                uint32_t lj = Ln[0];
+#pragma unroll
+                for (int i = 1; i < M; ++i) lj = (j == (uint32_t)i) ? Ln[i] : lj;
+                uint4 x = v[k];
+                if (c < 5u) fhdr[wv][j][c] = x;  // the plan's first 80 bytes
+                if (16u * c + 16u > lj) {        // the frame's last chunk: bytes >= len out
+                    const uint32_t t = lj - 1u, o = 16u * c;
+                    ftail[wv][j] = (comp(x, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu;
+                    const uint32_t keep = lj - o;  // 1..15
+                    x.x &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+                    x.y &= keep >= 8 ? 0xFFFFFFFFu : (keep <= 4 ? 0u : ((1u << (8 * (keep - 4))) - 1u));
+                    x.z &= keep >= 12 ? 0xFFFFFFFFu : (keep <= 8 ? 0u : ((1u << (8 * (keep - 8))) - 1u));
+                    x.w &= keep <= 12 ? 0u : ((1u << (8 * (keep - 12))) - 1u);
+                }
+                a = add_chunk(x, 0u);
+            }
+            // j is non-decreasing across lanes: a row whose first and last lanes share j is all
+            // one packet, and adds its row sum with one LDS atomic instead of 16
+            const uint32_t jf = row_bcast<0, 16>(j), jl = row_bcast<15, 16>(j);
+            const uint32_t rs_ = row_sum<16>(a);
+            if (jf == jl) {
+                if (rl == 0 && j != 0xFFFFu) atomicAdd(&fsum[wv][j], rs_);
+            } else if (j != 0xFFFFu) {
+                atomicAdd(&fsum[wv][j], a);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (!valid) return;
+    // lane j plans packet j from the header buffer (chunks past the frame read as zeros)
+    uint32_t h[20];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint4 c = ((uint32_t)k < nch) ? fhdr[wv][lane][k] : make_uint4(0u, 0u, 0u, 0u);
+        h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
+    }
+    RPlan Q = lane_plan(h, len);
+    uint32_t l4w = NFCS_PATCH_NONE;
+    bool done = false;
+    if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
+        Q = slow_plan(frame, len);
+        if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
+            const SeqOut o = seq_update(frame, len);
+            Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
+            Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
+            l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
+            done = true;
+        }
+    }
+    if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
+    if (!done && (Q.flags & F_L4)) {
+        // whole-frame sum minus the dwords below lo4, minus the bytes past re, + odd tail
+        const uint32_t lo4 = Q.rs & ~3u, re = Q.re;
+        uint32_t z = fsum[wv][lane] + Q.corr;
+#pragma unroll
+        for (uint32_t q = 0; q < 20; ++q) z -= wsum((4u * q < lo4) ? h[q] : 0u, 0u);
+        uint32_t tb;
+        if (re < len) {  // frame longer than its L4 region (rare): from memory
+            z -= sum_bytes_le(frame, re, len);
+            tb = frame[re - 1u];
+        } else {
+            tb = ftail[wv][lane];
+        }
+        if (Q.flags & F_TAIL) z += 255u * tb;
+        uint32_t c = (~fold32(z)) & 0xFFFFu;
+        if ((Q.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
+        l4w = Q.fs | (c << 16);
+    }
+    const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
+    if (!(DBG & 1) && live && !done) {
+        if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) {
+            frame[ipw & 0xFFFFu] = (uint8_t)(ipw >> 16);
+            frame[(ipw & 0xFFFFu) + 1] = (uint8_t)(ipw >> 24);
+        }
+        if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) {
+            frame[l4w & 0xFFFFu] = (uint8_t)(l4w >> 16);
+            frame[(l4w & 0xFFFFu) + 1] = (uint8_t)(l4w >> 24);
+        }
+    }
+    if (status) status[p] = (uint8_t)Q.st;
+    if (patch) {
+        uint2 pr;
+        pr.x = (ipw & 0xFFFFu) | (l4w << 16);
+        pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
+        ((uint2*)patch)[p] = pr;
+    }
+}
+
 #endif  // NFCS_EXPERIMENTS
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
@@ -1466,6 +1642,15 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         break;
     }
 #ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+#define NFCS_FLAT(K, M)                                                                           \
+    hipLaunchKernelGGL((update_flat_kernel<K, M, 0>), dim3((n + 4u * M - 1u) / (4u * M)), dim3(kBlock), \
+                       0, stream, arena, arena_bytes, desc, n, base16, status, patch)
+    case 44: NFCS_FLAT(6, 4); break;
+    case 45: NFCS_FLAT(6, 5); break;
+    case 46: NFCS_FLAT(6, 6); break;
+    case 48: NFCS_FLAT(8, 8); break;
+    case 43: NFCS_FLAT(6, 3); break;
+#undef NFCS_FLAT
     case 40: hipLaunchKernelGGL((update_win_kernel<6, 16, 64, 0, 6>), dim3((n + 255u) / 256u),
                                 dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch); break;  // window mode (flat stream per wave), K=6
