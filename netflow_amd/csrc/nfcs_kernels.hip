@@ -1029,8 +1029,12 @@ __global__ __launch_bounds__(kBlock, 1) void update_lp_kernel(uint8_t* __restric
         // hoisted out of the loop into long-lived VGPRs
         uint32_t rlv = rl;
         asm volatile("" : "+v"(rlv));
-        S.idx = it * PR + row;
+        // issued unconditionally (past the last step: dummy loads), so the compiler can wait for
+        // the previous stage with a counted vmcnt instead of draining this one too
+        const bool on = it < iters;
+        S.idx = on ? it * PR + row : 0u;
         S.r0 = sh.rec[wv][S.idx][0];
+        if (!on) S.r0.y = 0u;
         const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
         const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
         // chunks 0 .. nre-1 in full (chunks past the region read zeros)
@@ -1109,10 +1113,10 @@ __global__ __launch_bounds__(kBlock, 1) void update_lp_kernel(uint8_t* __restric
     Stage A, B;
     stage(A, 0);
     for (uint32_t it = 0; it < iters; it += 2) {
-        if (it + 1 < iters) stage(B, it + 1);
+        stage(B, it + 1);
         finish(A);
         if (it + 1 >= iters) break;
-        if (it + 2 < iters) stage(A, it + 2);
+        stage(A, it + 2);
         finish(B);
     }
 }
@@ -1323,8 +1327,12 @@ __global__ __launch_bounds__(kBlock, 1) void update_win_kernel(uint8_t* __restri
         // hoisted out of the loop into long-lived VGPRs
         uint32_t rlv = rl;
         asm volatile("" : "+v"(rlv));
-        S.idx = it * PR + row;
+        // issued unconditionally (past the last step: dummy loads), so the compiler can wait for
+        // the previous stage with a counted vmcnt instead of draining this one too
+        const bool on = it < iters;
+        S.idx = on ? it * PR + row : 0u;
         S.r0 = sh.rec[wv][S.idx][0];
+        if (!on) S.r0.y = 0u;
         const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
         const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
         // chunks 0 .. nre-1 in full (chunks past the region read zeros)
@@ -1403,10 +1411,10 @@ __global__ __launch_bounds__(kBlock, 1) void update_win_kernel(uint8_t* __restri
     Stage A, B;
     stage(A, 0);
     for (uint32_t it = 0; it < iters; it += 2) {
-        if (it + 1 < iters) stage(B, it + 1);
+        stage(B, it + 1);
         finish(A);
         if (it + 1 >= iters) break;
-        if (it + 2 < iters) stage(A, it + 2);
+        stage(A, it + 2);
         finish(B);
     }
 }
