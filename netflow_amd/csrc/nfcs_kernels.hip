@@ -798,6 +798,41 @@ __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __res
     }
 }
 
+// Grid-stride form with one group of look-ahead: a wave processes its 4-packet groups in a loop
+// and issues the next group's descriptors and loads before it processes the current one, so its
+// loads are in flight through its own compute and stores (C3 is memory-parallelism bound:
+// DESIGN.md §5b). Every stage is issued unconditionally (past the end: dummy loads) so the
+// compiler waits for the current group with a counted vmcnt.
+template <int K, int NT, int R = 16, int SV = 1>
+__global__ __launch_bounds__(kBlock, 1) void update_rows_pipe_kernel(uint8_t* __restrict__ arena,
+                                                                     uint64_t arena_bytes,
+                                                                     const nfcs_desc* __restrict__ desc,
+                                                                     uint32_t n, uint32_t base16,
+                                                                     uint8_t* __restrict__ status,
+                                                                     nfcs_patch* __restrict__ patch) {
+    constexpr uint32_t PW = 64 / R;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t stride = (uint64_t)gridDim.x * (kBlock / R);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    if (w0 >= n) return;
+    RowStage<K> A, B;
+    auto stage = [&](RowStage<K>& S, uint64_t pw) {
+        const DescW<PW> D = load_descw<PW>(desc, pw < n ? pw : w0, n);
+        nfcs_desc d = pick_desc<PW>(D, row);
+        row_stage<K, NT, R, false>(S, arena, arena_bytes, d, pw < n ? pw + row : (uint64_t)n, n,
+                                   base16, rl);
+    };
+    stage(A, w0);
+    for (uint64_t pw = w0; pw < n; pw += 2 * stride) {
+        stage(B, pw + stride);
+        row_process<K, NT, 0, R, false, SV>(A, rl, rowbase4, status, patch, 0);
+        if (pw + stride >= n) break;
+        stage(A, pw + 2 * stride);
+        row_process<K, NT, 0, R, false, SV>(B, rl, rowbase4, status, patch, 0);
+    }
+}
+
 // Split mode, second pass: write the patch records of the checksum pass into the frames. A
 // write-only pass over 8 bytes per packet, so the frame stream of the first pass carries no
 // scattered stores (each write transaction in a read stream costs far more than its bytes).
@@ -1650,6 +1685,15 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         break;
     }
 #ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+    case 50: case 51: case 52: case 53: {  // pipelined row kernel, grid = waves per SIMD x SIMDs
+        const int wps = variant - 48;        // 2..5 waves per SIMD
+        const uint32_t need = (n + 15u) / 16u;
+        uint32_t g = (uint32_t)(di.cus * wps);
+        if (g > need) g = need;
+        hipLaunchKernelGGL((update_rows_pipe_kernel<6, 2, 16, 1>), dim3(g), dim3(kBlock), 0, stream,
+                           arena, arena_bytes, desc, n, base16, status, patch);
+        break;
+    }
 #define NFCS_FLAT(K, M)                                                                           \
     hipLaunchKernelGGL((update_flat_kernel<K, M, 0>), dim3((n + 4u * M - 1u) / (4u * M)), dim3(kBlock), \
                        0, stream, arena, arena_bytes, desc, n, base16, status, patch)
