@@ -1754,7 +1754,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     const uint32_t need = (n + 15u) / 16u;
     const int g = grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
     const FwdArgs fa = {nh, table, table_n};
-    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, true>), dim3(g), dim3(kBlock), 0, stream,
+    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, true, 1>), dim3(g), dim3(kBlock), 0, stream,
                        arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa);
     return hipGetLastError();
 }
