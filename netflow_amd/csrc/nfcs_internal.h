@@ -45,6 +45,10 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 // the same store in its own pass. The default variant picks it when the mean
 // arena footprint per packet is at least kSplitMeanBytes.
 constexpr uint64_t kSplitMeanBytes = 2048;
+// Below this mean footprint per packet the default kernel runs in one-wave workgroups: short
+// frames make short-lived waves, and single-wave workgroups retire and relaunch them with less
+// granularity loss (C3 +2-3%, profiles/r01_s2_variants.md run bs1/bs2).
+constexpr uint64_t kSmallMeanBytes = 1200;
 inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
     return variant == 8 || variant == 22 || variant == 23 ||  // 22/23: experiments build only
            (variant == 0 && n > 0 && arena_bytes / n >= kSplitMeanBytes);

@@ -763,8 +763,9 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 
 // Grid-stride over packets (the default grid has one workgroup per 4*64/R packets, so no
 // loop), 64/R packet rows per wave.
-template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false, int SV = 0>
-__global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
+template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false, int SV = 0,
+          int BS = kBlock>
+__global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
                                                                   uint64_t arena_bytes,
                                                                   const nfcs_desc* __restrict__ desc,
                                                                   uint32_t n, uint32_t base16,
@@ -774,8 +775,8 @@ __global__ __launch_bounds__(kBlock, OCC) void update_rows_kernel(uint8_t* __res
     constexpr uint32_t PW = 64 / R;  // packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint32_t stride = gridDim.x * (kBlock / R);
-    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    const uint32_t stride = gridDim.x * (BS / R);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (BS / R) + rfl(threadIdx.x >> 6) * PW;
     if (w0 >= n) return;
     DescW<PW> Dn = load_descw<PW>(desc, w0, n);
     for (uint64_t pw = w0; pw < n; pw += stride) {
@@ -1639,6 +1640,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     nfcs_patch* ws = work.patch;
     if (n == 0) return hipSuccess;
     if (variant == 0 && use_split(0, arena_bytes, n)) variant = 8;  // large frames: split mode
+    if (variant == 0 && arena_bytes / n < kSmallMeanBytes) variant = 29;  // short frames: 1-wave WGs
     // One workgroup per 4*64/R packets, as many workgroups as that takes (a grid that
     // grid-strides over resident workgroups measured 10-15% slower: DESIGN.md §5).
     auto rows_grid = [&](int R) {
@@ -1662,6 +1664,11 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                                 dim3(kBlock), di.lds_pad, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;
     case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
+    case 29:  // as 0 in one-wave workgroups (4 packets each): measured +2-3% on C3, -0.7% on C1
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, 64>), dim3((n + 3u) / 4u),
+                           dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
+                           nofwd);
+        break;
     case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
     case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
     case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
@@ -1685,6 +1692,15 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         break;
     }
 #ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+#define NFCS_ROWS_BS(BS)                                                                          \
+    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, BS>),                         \
+                       dim3((n + (BS / 16) - 1) / (BS / 16)), dim3(BS), 0, stream, arena, arena_bytes, \
+                       desc, n, base16, status, patch, nofwd)
+    case 60: NFCS_ROWS_BS(64); break;    // default kernel, one wave per workgroup
+    case 61: NFCS_ROWS_BS(128); break;
+    case 62: NFCS_ROWS_BS(512); break;
+    case 63: NFCS_ROWS_BS(1024); break;
+#undef NFCS_ROWS_BS
     case 50: case 51: case 52: case 53: {  // pipelined row kernel, grid = waves per SIMD x SIMDs
         const int wps = variant - 48;        // 2..5 waves per SIMD
         const uint32_t need = (n + 15u) / 16u;
