@@ -799,41 +799,6 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     }
 }
 
-// Grid-stride form with one group of look-ahead: a wave processes its 4-packet groups in a loop
-// and issues the next group's descriptors and loads before it processes the current one, so its
-// loads are in flight through its own compute and stores (C3 is memory-parallelism bound:
-// DESIGN.md §5b). Every stage is issued unconditionally (past the end: dummy loads) so the
-// compiler waits for the current group with a counted vmcnt.
-template <int K, int NT, int R = 16, int SV = 1>
-__global__ __launch_bounds__(kBlock, 1) void update_rows_pipe_kernel(uint8_t* __restrict__ arena,
-                                                                     uint64_t arena_bytes,
-                                                                     const nfcs_desc* __restrict__ desc,
-                                                                     uint32_t n, uint32_t base16,
-                                                                     uint8_t* __restrict__ status,
-                                                                     nfcs_patch* __restrict__ patch) {
-    constexpr uint32_t PW = 64 / R;
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
-    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t stride = (uint64_t)gridDim.x * (kBlock / R);
-    const uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
-    if (w0 >= n) return;
-    RowStage<K> A, B;
-    auto stage = [&](RowStage<K>& S, uint64_t pw) {
-        const DescW<PW> D = load_descw<PW>(desc, pw < n ? pw : w0, n);
-        nfcs_desc d = pick_desc<PW>(D, row);
-        row_stage<K, NT, R, false>(S, arena, arena_bytes, d, pw < n ? pw + row : (uint64_t)n, n,
-                                   base16, rl);
-    };
-    stage(A, w0);
-    for (uint64_t pw = w0; pw < n; pw += 2 * stride) {
-        stage(B, pw + stride);
-        row_process<K, NT, 0, R, false, SV>(A, rl, rowbase4, status, patch, 0);
-        if (pw + stride >= n) break;
-        stage(A, pw + 2 * stride);
-        row_process<K, NT, 0, R, false, SV>(B, rl, rowbase4, status, patch, 0);
-    }
-}
-
 // Split mode, second pass: write the patch records of the checksum pass into the frames. A
 // write-only pass over 8 bytes per packet, so the frame stream of the first pass carries no
 // scattered stores (each write transaction in a read stream costs far more than its bytes).
@@ -861,776 +826,7 @@ __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restri
 }
 
 #ifdef NFCS_EXPERIMENTS  // measured alternatives, measurement builds only
-// =============================================================================================
-// v4: lane-per-packet planning, row-per-packet summing.
-//
-// PMC (profiles/r01_pmc_per_packet.json) put v3 at ~103 VALU wave-instructions per packet, i.e.
-// ~65% of the VALU issue capacity on C1 and all of it on C3 (4 cycles per wave64 VALU op): the
-// per-packet header plan, executed by a 16-lane row, costs one wave instruction per four
-// packets. Here a wave owns P = 64 consecutive packets:
-//   phase A  lane j plans packet j alone: its 8-byte descriptor (one coalesced load for the
-//            wave), the first 80 header bytes in 20 registers (five 16-byte loads; an 802.1Q
-//            tag is one select per dword), then update_checksums()'s decisions at compile-time
-//            offsets, so one VALU instruction plans 64 packets. Uncommon headers call the
-//            lane-0-style slow planner (IP options) or the exact sequential emulation (IHL < 5)
-//            in their own lane. The plan goes to LDS as an 8-dword record.
-//   phase B  16-lane rows (four packets per wave instruction) stream the summed region of
-//            each packet exactly as v3 does (6 slots of 16-byte loads per lane, jumbo frames in
-//            further batches), the next four packets' record and loads in flight while the
-//            current four are summed, folded and written back.
-// =============================================================================================
-struct LaneHdr {  // view dwords of the first 80 frame bytes, 802.1Q tag removed for bytes >= 12
-    uint32_t d[20];
-    DEV uint32_t b(uint32_t o) const { return (d[o >> 2] >> (8 * (o & 3u))) & 0xFFu; }
-    DEV uint32_t le16(uint32_t o) const { return (d[o >> 2] >> (8 * (o & 2u))) & 0xFFFFu; }
-    DEV uint32_t be16(uint32_t o) const { return bswap16(le16(o)); }
-};
-
-// packet.hpp:773-889 in view coordinates for a compile-time l4 (34: IPv4 IHL 5, 54: IPv6).
-template <uint32_t L4>
-DEV RPlan lane_l4(const LaneHdr& V, RPlan P, uint32_t lenv, uint32_t v4, uint32_t proto, uint32_t sh) {
-    const uint32_t skip = v4 ? NFCS_ST_V4_L4SKIP : NFCS_ST_V6_L4SKIP;
-    uint32_t L = 0, st = 0, fl = F_L4, sub = (L4 & 2u) ? V.le16(L4 - 2) : 0u, fs = 0;
-    // sub: the LE word before an l4 at 2 mod 4 (sh = 4 keeps the parity) and the raw bytes of
-    // the checksum field the reference zeroes first (795 / 838 / 885)
-    auto field = [&](uint32_t FS, uint32_t re) {
-        uint32_t s = 0;
-        if (FS < re) s += V.b(FS) << ((FS & 1u) ? 8 : 0);
-        if (FS + 1 < re) s += V.b(FS + 1) << (((FS + 1) & 1u) ? 8 : 0);
-        return s;
-    };
-    if (proto == 6) {
-        if (L4 + 19 > lenv) { P.st = skip; return P; }  // sizeof(TcpHeader) == 19
-        const uint32_t hl = (V.b(L4 + 12) >> 4) * 4u;
-        if (v4) {
-            const uint32_t tl = V.be16(16);
-            if (tl < 20u) { P.st = skip; return P; }
-            L = (tl - 20u) & 0xFFFFu;
-        } else {
-            L = V.be16(18);
-        }
-        if (L < hl || L4 + L > lenv) { P.st = skip; return P; }
-        fs = L4 + 15;  // TcpHeader::checksum at offset 15 (19-byte packed struct)
-        sub += field(L4 + 15, L4 + L);
-        st = v4 ? NFCS_ST_V4_TCP : NFCS_ST_V6_TCP;
-    } else if (proto == 17) {
-        if (L4 + 8 > lenv) { P.st = skip; return P; }
-        L = V.be16(L4 + 4);
-        if (L < 8 || L4 + L > lenv) { P.st = skip; return P; }
-        fs = L4 + 6;
-        sub += field(L4 + 6, L4 + L);
-        fl |= F_UDP;
-        st = v4 ? NFCS_ST_V4_UDP : NFCS_ST_V6_UDP;
-    } else if (proto == 1 && v4) {
-        if (L4 + 8 > lenv) { P.st = skip; return P; }
-        const uint32_t tl = V.be16(16);
-        if (tl < 20u) { P.st = skip; return P; }
-        L = tl - 20u;
-        if (L4 + L > lenv || L < 8) { P.st = skip; return P; }
-        fs = L4 + 2;
-        sub += field(L4 + 2, L4 + L);
-        st = NFCS_ST_V4_ICMP;
-    } else {
-        return P;
-    }
-    uint32_t add = 0;
-    if (proto != 1) {  // pseudo-header in the LE domain (797-816 / 840-859)
-        add = bswap16(proto) + bswap16(L);
-        if (v4) {
-            add += V.le16(26) + V.le16(28) + V.le16(30) + V.le16(32);
-        } else {
-#pragma unroll
-            for (uint32_t w = 0; w < 32; w += 2) add += V.le16(22 + w);
-        }
-    }
-    const uint32_t re = L4 + L, t = re - 1;
-    if ((L & 1u) && !(t >= fs && t < fs + 2)) fl |= F_TAIL;
-    P.st = st;
-    P.flags |= fl;
-    P.rs = L4 + sh;
-    P.re = re + sh;
-    P.fs = fs + sh;
-    P.corr = add - sub;
-    return P;
-}
-
-// fast_plan on one lane's registers: h = frame dwords 0..19 (bytes >= len may hold anything).
-DEV RPlan lane_plan(const uint32_t (&h)[20], uint32_t len) {
-    const bool tagged = (len >= 14) && bswap16(h[3] & 0xFFFFu) == 0x8100u;  // ethernet(): l2 = 18
-    const uint32_t sh = tagged ? 4u : 0u;
-    LaneHdr V;
-#pragma unroll
-    for (int i = 0; i < 20; ++i) V.d[i] = (i < 3) ? h[i] : (i < 19 ? (tagged ? h[i + 1] : h[i]) : (tagged ? 0u : h[i]));
-    const uint32_t lenv = len - sh;
-    const uint32_t b0 = V.b(14);
-    if (len >= 14 + sh && lenv >= 34 && (b0 >> 4) == 4) {  // 728-734: IPv4 by nibble
-        if ((b0 & 15u) != 5) return rplan_none(NFCS_ST_NONE | (F_SEQ << 8));
-        // 739-740: header checksum, field (view 24-25) zeroed: LE words of view bytes 14..33
-        uint32_t s = (V.d[3] >> 16) + (V.d[8] & 0xFFFFu);
-        s = wsum(V.d[4], wsum(V.d[5], wsum(V.d[6] & 0xFFFF0000u, wsum(V.d[7], s))));
-        RPlan P = rplan_none(NFCS_ST_V4);
-        P.flags = F_IP;
-        P.ipw = (24u + sh) | (((~fold32(s)) & 0xFFFFu) << 16);
-        return lane_l4<34>(V, P, lenv, 1u, V.b(23), sh);
-    }
-    // 741-765: effective EtherType (after one tag) must be IPv6 and the nibble 6
-    const uint32_t et = (len >= 14 + sh) ? V.be16(12) : 0u;
-    if (et != 0x86DDu || !(len >= 14 + sh && lenv >= 54 && (b0 >> 4) == 6))
-        return rplan_none(NFCS_ST_NONE);
-    return lane_l4<54>(V, rplan_none(NFCS_ST_V6), lenv, 0u, V.b(20), sh);
-}
-
-// Plan record in LDS, 8 dwords per packet.
-enum : uint32_t { RF_LIVE = 1u << 29, RF_DONE = 1u << 30 };  // in r[1] with flags << 24
-struct LRec { uint32_t off16, re_fl, rs_fs, corr, ipw, st, l4w, pad; };
-
-template <int P>
-struct LpShared { uint4 rec[kWavesPerBlock][P][2]; };
-
-template <int K, int R, int P, int DBG>
-__global__ __launch_bounds__(kBlock, 1) void update_lp_kernel(uint8_t* __restrict__ arena,
-                                                              uint64_t arena_bytes,
-                                                              const nfcs_desc* __restrict__ desc,
-                                                              uint32_t n, uint32_t base16,
-                                                              uint8_t* __restrict__ status,
-                                                              nfcs_patch* __restrict__ patch) {
-    static_assert(P == 64, "one plan lane per packet");
-    __shared__ LpShared<P> sh;
-    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
-    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * P;
-    if (pw >= n) return;
-    // ---- phase A: lane `lane` plans packet pw + lane -----------------------------------------
-    {
-        const uint64_t p = pw + lane;
-        const bool valid = p < n;
-        const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
-        const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
-        const bool bad = valid && ((d.off16 < base16) ||
-                                   (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
-        const bool live = valid && !bad;
-        const uint32_t len = live ? d.len : 0u;
-        uint8_t* frame = arena + (live ? off : 0);
-        const uint32_t nch = (len + 15u) >> 4;
-        uint32_t h[20];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint4 c = ld16<0>(((uint32_t)k < nch) ? (const uint4*)frame + k : &g_zero16);
-            h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
-        }
-        RPlan Q = lane_plan(h, len);
-        uint32_t l4w = NFCS_PATCH_NONE, done = 0;
-        if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
-            Q = slow_plan(frame, len);
-            if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
-                const SeqOut o = seq_update(frame, len);
-                Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
-                Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
-                l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
-                done = RF_DONE;
-            }
-        }
-        if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
-        const uint32_t re = (Q.flags & F_L4) ? Q.re : 0u;
-        // phase B sums whole chunks from chunk 0: the frame dwords below lo4 = rs & ~3 (all in
-        // h: rs <= l2 + 60 < 80) are subtracted here once, so no chunk needs a start mask
-        {
-            const uint32_t lo4 = Q.rs & ~3u;
-            uint32_t hs = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 20; ++q) hs = wsum((4u * q < lo4) ? h[q] : 0u, hs);
-            if (re) Q.corr -= hs;
-        }
-        const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
-        uint4* r = sh.rec[wv][lane];
-        r[0] = make_uint4(live ? (uint32_t)(off >> 4) : 0u, re | (Q.flags << 24) | (valid ? RF_LIVE : 0u) | done,
-                          (Q.rs & 0xFFFFu) | (Q.fs << 16), Q.corr);
-        r[1] = make_uint4(ipw, Q.st, l4w, 0u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    // ---- phase B: rows of R lanes sum their packet's region --------------------------------
-    constexpr uint32_t PR = 64 / R;  // packets per wave instruction
-    const uint32_t rl = lane & (R - 1), row = lane / R;
-    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
-    const uint32_t iters = (cnt + PR - 1) / PR;
-
-    struct Stage {
-        uint4 v[K];
-        uint4 t;   // the region's last chunk (end excess, odd-tail byte)
-        uint4 r0;  // off16, re | flags, rs | fs, corr (header prefix folded in)
-        uint32_t idx;
-    };
-    auto stage = [&](Stage& S, uint32_t it) {
-        // rlv is opaque in every iteration, so per-slot offsets are recomputed rather than
-        // hoisted out of the loop into long-lived VGPRs
-        uint32_t rlv = rl;
-        asm volatile("" : "+v"(rlv));
-        // issued unconditionally (past the last step: dummy loads), so the compiler can wait for
-        // the previous stage with a counted vmcnt instead of draining this one too
-        const bool on = it < iters;
-        S.idx = on ? it * PR + row : 0u;
-        S.r0 = sh.rec[wv][S.idx][0];
-        if (!on) S.r0.y = 0u;
-        const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
-        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
-        // chunks 0 .. nre-1 in full (chunks past the region read zeros)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t c = rlv + (uint32_t)R * k;
-            const uint4* a = (c < nre) ? src + c : &g_zero16;
-            S.v[k] = (k == 0) ? ld16<0>(a) : ld16<1>(a);
-        }
-        S.t = ld16<0>(nre ? src + (nre - 1u) : &g_zero16);
-    };
-    auto finish = [&](const Stage& S) {
-        uint32_t rlv = rl;
-        asm volatile("" : "+v"(rlv));
-        const uint32_t fl = (S.r0.y >> 24) & 0x1Fu;
-        const uint32_t re = S.r0.y & 0x1FFFFu, fs = S.r0.z >> 16;
-        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc = add_chunk(S.v[k], acc);
-        const uint32_t nre = (re + 15u) >> 4;
-        const uint32_t cmax = wave_max_rows<R>(nre);
-        // jumbo frames: the rest in batches of K2 slots (the next stage's K slots are in flight,
-        // so a K-slot batch here would cost 30 VGPRs for the whole kernel)
-        constexpr int K2 = 2;
-        for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K2) {
-            uint4 w[K2];
-#pragma unroll
-            for (int k = 0; k < K2; ++k) {
-                const uint32_t c = cb + rlv + (uint32_t)R * k;
-                w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
-            }
-#pragma unroll
-            for (int k = 0; k < K2; ++k) acc = add_chunk(w[k], acc);
-        }
-        if (rl == 0 && re) {  // the last chunk's bytes past re; the odd trailing byte (903-905)
-            const uint32_t o = (re - 1u) & ~15u;
-            uint32_t ex = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const int nb = (int)re - (int)(o + 4u * j);
-                const uint32_t m = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
-                ex = wsum(comp(S.t, j) & m, ex);
-            }
-            acc -= ex;
-            const uint32_t t = re - 1u;
-            if (fl & F_TAIL) acc += 255u * ((comp(S.t, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
-        }
-        const uint32_t z = row_sum<R>(acc) + S.r0.w;
-        const uint4 r1 = sh.rec[wv][S.idx][1];
-        const bool done = S.r0.y & RF_DONE, live = S.r0.y & RF_LIVE;
-        uint32_t l4w = r1.z;
-        if (!done && (fl & F_L4)) {
-            uint32_t c = (~fold32(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
-            if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
-            l4w = fs | (c << 16);
-        }
-        const uint32_t ipw = r1.x;
-        uint8_t* frame = arena + (uint64_t)S.r0.x * 16u;
-        if (!(DBG & 1) && live && !done && rl < 4) {
-            const uint32_t w = (rl & 2u) ? l4w : ipw;
-            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
-        }
-        if (live && rl == 0) {
-            const uint64_t p = pw + S.idx;
-            if (status) status[p] = (uint8_t)r1.y;
-            if (patch) {
-                uint2 pr;
-                pr.x = (ipw & 0xFFFFu) | (l4w << 16);
-                pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
-                ((uint2*)patch)[p] = pr;
-            }
-        }
-    };
-    Stage A, B;
-    stage(A, 0);
-    for (uint32_t it = 0; it < iters; it += 2) {
-        stage(B, it + 1);
-        finish(A);
-        if (it + 1 >= iters) break;
-        stage(A, it + 2);
-        finish(B);
-    }
-}
-
-template <int K, int R, int P, int DBG, int KW>
-__global__ __launch_bounds__(kBlock, 1) void update_win_kernel(uint8_t* __restrict__ arena,
-                                                              uint64_t arena_bytes,
-                                                              const nfcs_desc* __restrict__ desc,
-                                                              uint32_t n, uint32_t base16,
-                                                              uint8_t* __restrict__ status,
-                                                              nfcs_patch* __restrict__ patch) {
-    static_assert(P == 64, "one plan lane per packet");
-    __shared__ LpShared<P> sh;
-    constexpr uint32_t MAXT = 6144;  // chunks of one wave's window: one map byte each
-    __shared__ __attribute__((aligned(16))) uint8_t wmap[kWavesPerBlock][MAXT];
-    __shared__ uint32_t wsums[kWavesPerBlock][P];
-    uint32_t w_start = 0, w_nre = 0, w_live = 0, w_ok = 1;  // this lane's packet, for the window
-    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
-    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * P;
-    if (pw >= n) return;
-    // ---- phase A: lane `lane` plans packet pw + lane -----------------------------------------
-    {
-        const uint64_t p = pw + lane;
-        const bool valid = p < n;
-        const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
-        const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
-        const bool bad = valid && ((d.off16 < base16) ||
-                                   (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
-        const bool live = valid && !bad;
-        const uint32_t len = live ? d.len : 0u;
-        uint8_t* frame = arena + (live ? off : 0);
-        const uint32_t nch = (len + 15u) >> 4;
-        uint32_t h[20];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint4 c = ld16<0>(((uint32_t)k < nch) ? (const uint4*)frame + k : &g_zero16);
-            h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
-        }
-        RPlan Q = lane_plan(h, len);
-        uint32_t l4w = NFCS_PATCH_NONE, done = 0;
-        if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
-            Q = slow_plan(frame, len);
-            if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
-                const SeqOut o = seq_update(frame, len);
-                Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
-                Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
-                l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
-                done = RF_DONE;
-            }
-        }
-        if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
-        const uint32_t re = (Q.flags & F_L4) ? Q.re : 0u;
-        // phase B sums whole chunks from chunk 0: the frame dwords below lo4 = rs & ~3 (all in
-        // h: rs <= l2 + 60 < 80) are subtracted here once, so no chunk needs a start mask
-        {
-            const uint32_t lo4 = Q.rs & ~3u;
-            uint32_t hs = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 20; ++q) hs = wsum((4u * q < lo4) ? h[q] : 0u, hs);
-            if (re) Q.corr -= hs;
-        }
-        const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
-        uint4* r = sh.rec[wv][lane];
-        r[0] = make_uint4(live ? (uint32_t)(off >> 4) : 0u, re | (Q.flags << 24) | (valid ? RF_LIVE : 0u) | done,
-                          (Q.rs & 0xFFFFu) | (Q.fs << 16), Q.corr);
-        r[1] = make_uint4(ipw, Q.st, l4w, 0u);
-        w_start = live ? (uint32_t)(off >> 4) : 0u;
-        w_nre = (re + 15u) >> 4;
-        w_live = live;
-        w_ok = !bad;
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    // ---- window mode: the wave's packets lie in arena order without gaps bigger than their
-    // regions: stream [W0, W0 + T) flat (chunk W0 + g in lane g % 64 of slot g / 64 — every
-    // lane's load useful, short frames or long), each chunk finds its packet in an LDS map
-    {
-        const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
-        const bool has = w_live && w_nre != 0;
-        const uint64_t hb = __builtin_amdgcn_ballot_w64(has);
-        bool ok = __builtin_amdgcn_ballot_w64(!w_ok) == 0 && hb != 0;
-        uint32_t W0 = 0, T = 0;
-        if (ok) {
-            const uint32_t first = (uint32_t)__builtin_ctzll(hb), last = 63u - (uint32_t)__builtin_clzll(hb);
-            W0 = (uint32_t)__builtin_amdgcn_readlane((int)w_start, (int)first);
-            T = (uint32_t)__builtin_amdgcn_readlane((int)(w_start + w_nre), (int)last) - W0;
-            // region lanes in ascending order: the previous region lanes' ends <= my start
-            uint32_t x = has ? (w_start + w_nre - W0) : 0u;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {  // inclusive running max over lanes
-                const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane >= (uint32_t)d) ? lane - d : lane) * 4u), (int)x);
-                x = (lane >= (uint32_t)d) ? max(x, y) : x;
-            }
-            uint32_t prev_end = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1u : 0u) * 4u), (int)x);
-            if (lane == 0) prev_end = 0;
-            const bool bad_order = has && (w_start < W0 || w_start - W0 < prev_end);
-            uint32_t dense = has ? w_nre : 0u;  // region chunks of the wave
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) dense += (uint32_t)__shfl_xor((int)dense, d);
-            ok = __builtin_amdgcn_ballot_w64(bad_order) == 0 && T <= MAXT && T <= 2u * dense + 64u;
-        }
-        if (ok) {
-            uint8_t* map = wmap[wv];
-            // map[g] = 0xFF (no region), j, or j | 0x40 on a region's last chunk
-            for (uint32_t q = lane; q < (T + 15u) >> 4; q += 64u)
-                ((uint4*)map)[q] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-            wsums[wv][lane] = 0;
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            if (has) {
-                const uint32_t a = w_start - W0, b = a + w_nre;  // map bytes [a, b)
-                const uint32_t jb = lane * 0x01010101u;
-                uint32_t c = a;
-                for (; c < b && (c & 3u); ++c) map[c] = (uint8_t)lane;
-                for (; c + 4 <= b; c += 4) *(uint32_t*)(map + c) = jb;
-                for (; c < b; ++c) map[c] = (uint8_t)lane;
-                map[b - 1] = (uint8_t)(lane | 0x40u);
-            }
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            const uint4* src = (const uint4*)arena + W0;
-            for (uint32_t g0 = 0; g0 < T; g0 += 64u * KW) {
-                uint4 v[KW];
-                uint32_t m[KW];
-#pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    const uint32_t g = g0 + 64u * k + lane;
-                    v[k] = ld16<1>((g < T) ? src + g : &g_zero16);
-                    m[k] = (g < T) ? map[g] : 0xFFu;
-                }
-#pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    if (m[k] != 0xFFu) {
-                        const uint32_t j = m[k] & 63u;
-                        uint32_t a = add_chunk(v[k], 0u);
-                        if (m[k] & 0x40u) {  // the region's last chunk: bytes past re, odd tail
-                            const uint4 r0 = sh.rec[wv][j][0];
-                            const uint32_t re = r0.y & 0x1FFFFu, o = (re - 1u) & ~15u;
-                            uint32_t ex = 0;
-#pragma unroll
-                            for (uint32_t jj = 0; jj < 4; ++jj) {
-                                const int nb = (int)re - (int)(o + 4u * jj);
-                                const uint32_t mk = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
-                                ex = wsum(comp(v[k], jj) & mk, ex);
-                            }
-                            a -= ex;
-                            const uint32_t t = re - 1u;
-                            if ((r0.y >> 24) & F_TAIL)
-                                a += 255u * ((comp(v[k], (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
-                        }
-                        atomicAdd(&wsums[wv][j], a);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("" ::: "memory");
-            // lane j: fold, write back, status / patch
-            if (lane < cnt) {
-                const uint4 r0 = sh.rec[wv][lane][0], r1 = sh.rec[wv][lane][1];
-                const uint32_t fl = (r0.y >> 24) & 0x1Fu, fs = r0.z >> 16;
-                const bool done = r0.y & RF_DONE, live = r0.y & RF_LIVE;
-                uint32_t l4w = r1.z;
-                if (!done && (fl & F_L4)) {
-                    uint32_t c = (~fold32(wsums[wv][lane] + r0.w)) & 0xFFFFu;
-                    if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
-                    l4w = fs | (c << 16);
-                }
-                const uint32_t ipw = r1.x;
-                uint8_t* frame = arena + (uint64_t)r0.x * 16u;
-                if (!(DBG & 1) && live && !done) {
-                    if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) {
-                        frame[ipw & 0xFFFFu] = (uint8_t)(ipw >> 16);
-                        frame[(ipw & 0xFFFFu) + 1] = (uint8_t)(ipw >> 24);
-                    }
-                    if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) {
-                        frame[l4w & 0xFFFFu] = (uint8_t)(l4w >> 16);
-                        frame[(l4w & 0xFFFFu) + 1] = (uint8_t)(l4w >> 24);
-                    }
-                }
-                if (live) {
-                    const uint64_t p = pw + lane;
-                    if (status) status[p] = (uint8_t)r1.y;
-                    if (patch) {
-                        uint2 pr;
-                        pr.x = (ipw & 0xFFFFu) | (l4w << 16);
-                        pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
-                        ((uint2*)patch)[p] = pr;
-                    }
-                }
-            }
-            return;
-        }
-    }
-    // ---- phase B: rows of R lanes sum their packet's region --------------------------------
-    constexpr uint32_t PR = 64 / R;  // packets per wave instruction
-    const uint32_t rl = lane & (R - 1), row = lane / R;
-    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)P ? (n - pw) : (uint64_t)P);
-    const uint32_t iters = (cnt + PR - 1) / PR;
-
-    struct Stage {
-        uint4 v[K];
-        uint4 t;   // the region's last chunk (end excess, odd-tail byte)
-        uint4 r0;  // off16, re | flags, rs | fs, corr (header prefix folded in)
-        uint32_t idx;
-    };
-    auto stage = [&](Stage& S, uint32_t it) {
-        // rlv is opaque in every iteration, so per-slot offsets are recomputed rather than
-        // hoisted out of the loop into long-lived VGPRs
-        uint32_t rlv = rl;
-        asm volatile("" : "+v"(rlv));
-        // issued unconditionally (past the last step: dummy loads), so the compiler can wait for
-        // the previous stage with a counted vmcnt instead of draining this one too
-        const bool on = it < iters;
-        S.idx = on ? it * PR + row : 0u;
-        S.r0 = sh.rec[wv][S.idx][0];
-        if (!on) S.r0.y = 0u;
-        const uint32_t nre = ((S.r0.y & 0x1FFFFu) + 15u) >> 4;
-        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
-        // chunks 0 .. nre-1 in full (chunks past the region read zeros)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t c = rlv + (uint32_t)R * k;
-            const uint4* a = (c < nre) ? src + c : &g_zero16;
-            S.v[k] = (k == 0) ? ld16<0>(a) : ld16<1>(a);
-        }
-        S.t = ld16<0>(nre ? src + (nre - 1u) : &g_zero16);
-    };
-    auto finish = [&](const Stage& S) {
-        uint32_t rlv = rl;
-        asm volatile("" : "+v"(rlv));
-        const uint32_t fl = (S.r0.y >> 24) & 0x1Fu;
-        const uint32_t re = S.r0.y & 0x1FFFFu, fs = S.r0.z >> 16;
-        const uint4* src = (const uint4*)(arena + (uint64_t)S.r0.x * 16u);
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc = add_chunk(S.v[k], acc);
-        const uint32_t nre = (re + 15u) >> 4;
-        const uint32_t cmax = wave_max_rows<R>(nre);
-        // jumbo frames: the rest in batches of K2 slots (the next stage's K slots are in flight,
-        // so a K-slot batch here would cost 30 VGPRs for the whole kernel)
-        constexpr int K2 = 2;
-        for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K2) {
-            uint4 w[K2];
-#pragma unroll
-            for (int k = 0; k < K2; ++k) {
-                const uint32_t c = cb + rlv + (uint32_t)R * k;
-                w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
-            }
-#pragma unroll
-            for (int k = 0; k < K2; ++k) acc = add_chunk(w[k], acc);
-        }
-        if (rl == 0 && re) {  // the last chunk's bytes past re; the odd trailing byte (903-905)
-            const uint32_t o = (re - 1u) & ~15u;
-            uint32_t ex = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const int nb = (int)re - (int)(o + 4u * j);
-                const uint32_t m = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
-                ex = wsum(comp(S.t, j) & m, ex);
-            }
-            acc -= ex;
-            const uint32_t t = re - 1u;
-            if (fl & F_TAIL) acc += 255u * ((comp(S.t, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
-        }
-        const uint32_t z = row_sum<R>(acc) + S.r0.w;
-        const uint4 r1 = sh.rec[wv][S.idx][1];
-        const bool done = S.r0.y & RF_DONE, live = S.r0.y & RF_LIVE;
-        uint32_t l4w = r1.z;
-        if (!done && (fl & F_L4)) {
-            uint32_t c = (~fold32(z)) & 0xFFFFu;  // LE-domain complement = bswap of ref value
-            if ((fl & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
-            l4w = fs | (c << 16);
-        }
-        const uint32_t ipw = r1.x;
-        uint8_t* frame = arena + (uint64_t)S.r0.x * 16u;
-        if (!(DBG & 1) && live && !done && rl < 4) {
-            const uint32_t w = (rl & 2u) ? l4w : ipw;
-            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
-        }
-        if (live && rl == 0) {
-            const uint64_t p = pw + S.idx;
-            if (status) status[p] = (uint8_t)r1.y;
-            if (patch) {
-                uint2 pr;
-                pr.x = (ipw & 0xFFFFu) | (l4w << 16);
-                pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
-                ((uint2*)patch)[p] = pr;
-            }
-        }
-    };
-    Stage A, B;
-    stage(A, 0);
-    for (uint32_t it = 0; it < iters; it += 2) {
-        stage(B, it + 1);
-        finish(A);
-        if (it + 1 >= iters) break;
-        stage(A, it + 2);
-        finish(B);
-    }
-}
-
-
-// ---- flat-M: M packets per wave laid back to back over 64 lanes x K slots ---------------------
-// A wave owns M consecutive packets (M from the batch's mean footprint, host-chosen). Flat
-// chunk g of the wave is chunk g - pre[j] of packet j, pre = exclusive prefix of the packets'
-// chunk counts: every lane's load is useful whatever the frame lengths, and all of them are
-// issued at wave start (no loop). The chunks are summed as soon as they land — whole frames,
-// bytes >= len masked — into an LDS sum per packet, so the chunk registers die before any
-// planning; the lanes holding a frame's first 80 bytes drop them into an LDS header buffer and
-// the lane holding its last chunk its last byte. Lane j then plans packet j from LDS
-// (lane_plan) and removes what lies outside the L4 region [rs, re) exactly: the frame dwords
-// below rs & ~3 from the header buffer, the bytes past re (rare: frames longer than their L4
-// length) from memory.
-DEV uint32_t sum_bytes_le(const uint8_t* f, uint32_t a, uint32_t b) {  // LE-word sum of [a, b)
-    uint32_t s = 0;
-    for (uint32_t o = a; o < b; ++o) s += (uint32_t)f[o] << ((o & 1u) ? 8 : 0);
-    return s;
-}
-
-template <int K, int M, int DBG>
-__global__ __launch_bounds__(kBlock, 1) void update_flat_kernel(uint8_t* __restrict__ arena,
-                                                                uint64_t arena_bytes,
-                                                                const nfcs_desc* __restrict__ desc,
-                                                                uint32_t n, uint32_t base16,
-                                                                uint8_t* __restrict__ status,
-                                                                nfcs_patch* __restrict__ patch) {
-    static_assert(M >= 1 && M <= 16, "packets per wave");
-    __shared__ uint32_t fsum[kWavesPerBlock][16];
-    __shared__ uint32_t ftail[kWavesPerBlock][16];
-    __shared__ uint4 fhdr[kWavesPerBlock][16][5];
-    const uint32_t lane = threadIdx.x & 63u, wv = rfl(threadIdx.x >> 6);
-    const uint64_t pw = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * M;
-    if (pw >= n) return;
-    const uint32_t cnt = (uint32_t)((n - pw) < (uint64_t)M ? (n - pw) : (uint64_t)M);
-    const bool valid = lane < cnt;
-    const uint64_t p = pw + lane;
-    const nfcs_desc d = valid ? desc[p] : nfcs_desc{0u, 0u};
-    const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
-    const bool bad = valid && ((d.off16 < base16) ||
-                               (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
-    const bool live = valid && !bad;
-    const uint32_t len = live ? d.len : 0u;
-    uint8_t* frame = arena + (live ? off : 0);
-    const uint32_t nch = (len + 15u) >> 4;
-    // exclusive prefix of the chunk counts, frame bases and lengths, as wave-uniform values
-    uint32_t P[M], Ln[M];
-    uint64_t F[M];
-    uint32_t T = 0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-        P[i] = T;
-        Ln[i] = (uint32_t)__builtin_amdgcn_readlane((int)len, i);
-        T += (Ln[i] + 15u) >> 4;
-        F[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)frame >> 32), i) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)frame, i);
-    }
-    if (lane < 16) {
-        fsum[wv][lane] = 0;
-        ftail[wv][lane] = 0;
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    // flat batches of K slots: slot k, lane l -> flat chunk g = cb + 64k + l
-    for (uint32_t cb = 0; cb < T; cb += 64u * K) {
-        uint4 v[K];
-        uint32_t cj[K];  // c | j << 16, 0xFFFF0000 past T
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t g = cb + 64u * k + lane;
-            uint32_t j = 0, pre = 0;
-            uint64_t base = F[0];
-#pragma unroll
-            for (int i = 1; i < M; ++i) {
-                const bool ge = g >= P[i];
-                j = ge ? (uint32_t)i : j;
-                pre = ge ? P[i] : pre;
-                base = ge ? F[i] : base;
-            }
-            const bool in = g < T;
-            v[k] = ld16<1>(in ? (const uint4*)base + (g - pre) : &g_zero16);
-            cj[k] = in ? ((g - pre) | (j << 16)) : 0xFFFF0000u;
-        }
-        const uint32_t rl = lane & 15u;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t j = cj[k] >> 16, c = cj[k] & 0xFFFFu;
-            uint32_t a = 0;
-            if (j != 0xFFFFu) {
-                uint32_t lj = Ln[0];
-#pragma unroll
-                for (int i = 1; i < M; ++i) lj = (j == (uint32_t)i) ? Ln[i] : lj;
-                uint4 x = v[k];
-                if (c < 5u) fhdr[wv][j][c] = x;  // the plan's first 80 bytes
-                if (16u * c + 16u > lj) {        // the frame's last chunk: bytes >= len out
-                    const uint32_t t = lj - 1u, o = 16u * c;
-                    ftail[wv][j] = (comp(x, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu;
-                    const uint32_t keep = lj - o;  // 1..15
-                    x.x &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
-                    x.y &= keep >= 8 ? 0xFFFFFFFFu : (keep <= 4 ? 0u : ((1u << (8 * (keep - 4))) - 1u));
-                    x.z &= keep >= 12 ? 0xFFFFFFFFu : (keep <= 8 ? 0u : ((1u << (8 * (keep - 8))) - 1u));
-                    x.w &= keep <= 12 ? 0u : ((1u << (8 * (keep - 12))) - 1u);
-                }
-                a = add_chunk(x, 0u);
-            }
-            // j is non-decreasing across lanes: a row whose first and last lanes share j is all
-            // one packet, and adds its row sum with one LDS atomic instead of 16
-            const uint32_t jf = row_bcast<0, 16>(j), jl = row_bcast<15, 16>(j);
-            const uint32_t rs_ = row_sum<16>(a);
-            if (jf == jl) {
-                if (rl == 0 && j != 0xFFFFu) atomicAdd(&fsum[wv][j], rs_);
-            } else if (j != 0xFFFFu) {
-                atomicAdd(&fsum[wv][j], a);
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    if (!valid) return;
-    // lane j plans packet j from the header buffer (chunks past the frame read as zeros)
-    uint32_t h[20];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const uint4 c = ((uint32_t)k < nch) ? fhdr[wv][lane][k] : make_uint4(0u, 0u, 0u, 0u);
-        h[4 * k] = c.x; h[4 * k + 1] = c.y; h[4 * k + 2] = c.z; h[4 * k + 3] = c.w;
-    }
-    RPlan Q = lane_plan(h, len);
-    uint32_t l4w = NFCS_PATCH_NONE;
-    bool done = false;
-    if (live && (Q.st >> 8) != 0) {  // uncommon header: this lane parses from memory
-        Q = slow_plan(frame, len);
-        if (Q.flags & F_SEQ) {  // IHL < 5 overlap: exact sequential emulation, all written
-            const SeqOut o = seq_update(frame, len);
-            Q = rplan_none(o.st | NFCS_ST_FLAG_OVERLAP);
-            Q.ipw = (o.ip_off & 0xFFFFu) | (o.ip_val << 16);
-            l4w = (o.l4_off & 0xFFFFu) | (o.l4_val << 16);
-            done = true;
-        }
-    }
-    if (!live) Q = rplan_none(bad ? (uint32_t)NFCS_ST_BAD_DESC : (uint32_t)NFCS_ST_NONE);
-    if (!done && (Q.flags & F_L4)) {
-        // whole-frame sum minus the dwords below lo4, minus the bytes past re, + odd tail
-        const uint32_t lo4 = Q.rs & ~3u, re = Q.re;
-        uint32_t z = fsum[wv][lane] + Q.corr;
-#pragma unroll
-        for (uint32_t q = 0; q < 20; ++q) z -= wsum((4u * q < lo4) ? h[q] : 0u, 0u);
-        uint32_t tb;
-        if (re < len) {  // frame longer than its L4 region (rare): from memory
-            z -= sum_bytes_le(frame, re, len);
-            tb = frame[re - 1u];
-        } else {
-            tb = ftail[wv][lane];
-        }
-        if (Q.flags & F_TAIL) z += 255u * tb;
-        uint32_t c = (~fold32(z)) & 0xFFFFu;
-        if ((Q.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
-        l4w = Q.fs | (c << 16);
-    }
-    const uint32_t ipw = done ? Q.ipw : ((Q.flags & F_IP) ? Q.ipw : NFCS_PATCH_NONE);
-    if (!(DBG & 1) && live && !done) {
-        if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) {
-            frame[ipw & 0xFFFFu] = (uint8_t)(ipw >> 16);
-            frame[(ipw & 0xFFFFu) + 1] = (uint8_t)(ipw >> 24);
-        }
-        if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) {
-            frame[l4w & 0xFFFFu] = (uint8_t)(l4w >> 16);
-            frame[(l4w & 0xFFFFu) + 1] = (uint8_t)(l4w >> 24);
-        }
-    }
-    if (status) status[p] = (uint8_t)Q.st;
-    if (patch) {
-        uint2 pr;
-        pr.x = (ipw & 0xFFFFu) | (l4w << 16);
-        pr.y = (ipw >> 16) | (l4w & 0xFFFF0000u);
-        ((uint2*)patch)[p] = pr;
-    }
-}
-
+#include "nfcs_experiments.inc"
 #endif  // NFCS_EXPERIMENTS
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
