@@ -373,13 +373,27 @@ def main():
     elif args.op == "flowkey":
         ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
                                           args.steps) / args.steps
-        want = None  # parity of the flow keys: tests/test_flow_keys.py (reference fixtures)
+        # parity: digest of the 64-byte records (they hold the hashes too) vs the reference's
+        gk = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json"))).get("flowkey_c1", {})
+        want = None
+        if first == 0 and n == gk.get("n") and args.align == gk.get("align"):
+            eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
+            rdesc = np.zeros(n, dtype=nf.DESC_DTYPE)
+            rdesc["off16"] = np.arange(n, dtype=np.uint32) * 4
+            rdesc["len"] = 64
+            d_rdesc = eng.alloc(rdesc.nbytes).upload(rdesc)
+            eng.sync()
+            got_fk = f"{eng.digest_device(d_keys, 64 * n, d_rdesc, n, 0):016x}"
+            want = gk["digest_records"]
+            d_rdesc.free()
     else:
         ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
         # parity of what was measured: digest of the updated arena vs the reference's
         want = golden_digest(args.config, first, n)
     achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
     got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
+    if args.op == "flowkey" and want is not None:
+        got = got_fk
     parity_ok = None if want is None else (got == want)
     parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
 

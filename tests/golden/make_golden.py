@@ -480,6 +480,39 @@ def make_configs(R):
         json.dump(res, fh, indent=1, sort_keys=True)
 
 
+def make_flowkey_c1(R):
+    """Digest of the reference's flow-key records (nfcs_flow_key layout) and hashes for C1 (1M
+    packets, 128-byte aligned frames): the records as an arena of 64-byte frames, hashes as
+    4-byte frames, each digested with DESIGN.md §6's order-independent digest."""
+    res = json.load(open(os.path.join(OUT, "configs.json")))
+    n = 1 << 20
+    M = (1 << 64) - 1
+    dr = dh = 0
+    for lo in range(0, n, CHUNK):
+        m = min(CHUNK, n - lo)
+        arena, desc = oracle.gen_config(1, CONFIG_SEED, lo, m, 128)
+        recs = np.zeros((m, 64), dtype=np.uint8)
+        hashes = np.zeros(m, dtype=np.uint32)
+        R.nfref_flow_keys_batch(oracle._ptr(arena), desc.ctypes.data, m, oracle._ptr(recs),
+                                oracle._ptr(hashes, oracle._u32p), 8)
+        rdesc = np.zeros(m, dtype=oracle.DESC_DTYPE)
+        rdesc["off16"] = np.arange(m, dtype=np.uint32) * 4
+        rdesc["len"] = 64
+        dr = (dr + oracle.digest(recs.reshape(-1), rdesc, lo)) & M
+        hdesc = np.zeros(m, dtype=oracle.DESC_DTYPE)
+        hb = np.zeros((m, 16), dtype=np.uint8)
+        hb[:, :4] = hashes.view(np.uint8).reshape(m, 4)
+        hdesc["off16"] = np.arange(m, dtype=np.uint32)
+        hdesc["len"] = 4
+        dh = (dh + oracle.digest(hb.reshape(-1), hdesc, lo)) & M
+    res["flowkey_c1"] = {"first": 0, "n": n, "align": 128, "digest_records": f"{dr:016x}",
+                         "digest_hashes": f"{dh:016x}",
+                         "how": "records as 64-byte frames at 64-byte stride; hashes as 4-byte frames at 16-byte stride"}
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+    print(f"flowkey C1 digests records {dr:016x} hashes {dh:016x}")
+
+
 def make_c4(R):
     """C4: 32M x 1500 B IPv4+UDP sharded across 8 GPUs, 4M packets per rank (weak scaling at
     1/2/4/8 GPUs): the reference's digest of every rank's shard."""
@@ -514,3 +547,5 @@ if __name__ == "__main__":
         make_vlan(R)
     if "c4" in what:
         make_c4(R)
+    if "flowkey_c1" in what:
+        make_flowkey_c1(R)
