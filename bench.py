@@ -229,12 +229,12 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
                       f"{threads} threads, g++ -O2, {el:.1f} s"}
 
 
-def load_traffic(config: int, n: int):
+def load_traffic(config: int, n: int, op: str = "update"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
     for the default batch size of the config; None otherwise."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        t = json.load(open(p)).get(f"C{config}")
+        t = json.load(open(p)).get(f"C{config}" + ("" if op == "update" else f"_{op}"))
     except (OSError, ValueError):
         return None
     if not t or n != DEFAULT_PACKETS[config]:
@@ -397,7 +397,7 @@ def main():
     parity_ok = None if want is None else (got == want)
     parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    traffic = load_traffic(args.config, n) if args.op == "update" else None
+    traffic = load_traffic(args.config, n, args.op) if args.align == 128 else None
     fk = args.op == "flowkey"
     total_packets = D.sum(float(n))
     out = {

@@ -24,12 +24,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 
 
-def run_pass(out, cfg, counters, steps):
-    """One rocprofv3 pass with the given counters; median per counter over update launches."""
-    d = os.path.join(out, f"c{cfg}_{counters[0]}")
+KERNEL = {"update": "update_rows_kernel", "l3fwd": "update_rows_kernel", "vlan": "vlan_rows_kernel",
+          "flowkey": "flow_keys_kernel"}
+
+
+def run_pass(out, cfg, counters, steps, op="update"):
+    """One rocprofv3 pass with the given counters; median per counter over the op's launches."""
+    d = os.path.join(out, f"c{cfg}_{op}_{counters[0]}")
     cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu"]
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--op", op]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
@@ -39,11 +43,11 @@ def run_pass(out, cfg, counters, steps):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for row in csv.DictReader(open(os.path.join(root, f))):
-                    if "update_rows_kernel" in row["Kernel_Name"] and row["Counter_Name"] in vals:
+                    if KERNEL[op] in row["Kernel_Name"] and row["Counter_Name"] in vals:
                         vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     for c, v in vals.items():
         if not v:
-            raise SystemExit(f"no {c} samples for the update kernel in {d}")
+            raise SystemExit(f"no {c} samples for {KERNEL[op]} in {d}")
     return {c: statistics.median(v) for c, v in vals.items()}, min(len(v) for v in vals.values())
 
 
@@ -52,6 +56,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     ap.add_argument("--configs", type=int, nargs="+", default=[1, 2, 3])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--ops", nargs="+", default=["update"], choices=list(KERNEL))
+    ap.add_argument("--merge", help="existing traffic.json to extend")
     a = ap.parse_args()
     a.out = os.path.abspath(a.out)  # rocprofv3 runs with cwd /tmp
     os.makedirs(a.out, exist_ok=True)
@@ -60,21 +66,23 @@ def main():
                      "cross-check: TCC_EA0_RDREQ x 128 B (gfx950 read requests are whole 128-B "
                      "lines; the stock 64-B expression under-counts by the same factor 2), "
                      "EA0_WRREQ(_64B) write requests; median over launches of bench.py"}
-    for cfg in a.configs:
-        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps)
-        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps)
+    if a.merge:
+        res = json.load(open(a.merge))
+    for cfg, op in [(c, o) for o in a.ops for c in a.configs]:
+        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op)
+        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op)
         q, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
-                        a.steps)
-        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps)
+                        a.steps, op)
+        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op)
         fb, wb = 2 * f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
         rq = q["TCC_EA0_RDREQ_sum"]
         rb_req = rq * 128
-        res[f"C{cfg}"] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+        res[f"C{cfg}" + ("" if op == "update" else f"_{op}")] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                           "per_packet": (fb + wb) / PACKETS[cfg], "launches": min(nf_, nw),
                           "read_bytes_from_requests": rb_req, "read_requests": rq,
                           "write_requests": wq["TCC_EA0_WRREQ_sum"],
                           "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}
-        print(f"C{cfg}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
+        print(f"C{cfg} {op}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
               f"{wb / 1e6:.1f} MB in {wq['TCC_EA0_WRREQ_sum']:.0f} requests per launch", flush=True)
     with open(os.path.join(a.out, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
