@@ -521,7 +521,6 @@ struct RowStage {
     uint32_t p;
     uint32_t valid, bad;
     uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
-    uint32_t mac[3];  // ... and its 12 MAC bytes
 };
 
 // Fused L3 forward inputs (unused by the plain update).
@@ -547,14 +546,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     S.frame = arena + (live ? off : 0);
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
-    if (FWD) {  // the row's next-hop MACs, issued first so they land before the header slot
-        S.nh = nh;
-        const uint32_t* m = (nh < fa->table_n) ? (const uint32_t*)(fa->table + nh)
-                                               : (const uint32_t*)&g_zero16;
-        S.mac[0] = m[0];
-        S.mac[1] = m[1];
-        S.mac[2] = m[2];
-    }
+    if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
     // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -564,13 +556,17 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
         // the checksum chunks are written back; payload slots stream through as evict-first
         S.v[k] = (NT == 2 && k == 0) ? ld16<0>(a) : ld16<NT>(a);
     }
+    // all K loads issue before any use of the header slot: without this fence the scheduler
+    // hoists the forward decision's first DPP read above the last loads of the FWD kernel and
+    // waits for the header line (vmcnt) with half the row's loads not yet issued
+    if (FWD) __builtin_amdgcn_sched_barrier(0);
 }
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
 // (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
 template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false, int SV = 0>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
-                     nfcs_patch* patch, uint32_t table_n = 0) {
+                     nfcs_patch* patch, uint32_t table_n = 0, const uint32_t* wmac = nullptr) {
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
@@ -592,10 +588,19 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                   : (ttl <= 1 ? (uint32_t)NFCS_ST_TTL_EXPIRED
                               : (S.nh >= table_n ? (uint32_t)NFCS_ST_NO_ROUTE : 0u));
         fwd = live && fst == 0;
-        if (fwd && rl == 0) {  // dst_mac, src_mac (286-289)
-            h0.x = S.mac[0];
-            h0.y = S.mac[1];
-            h0.z = S.mac[2];
+        if (fwd && rl == 0) {  // dst_mac, src_mac (286-289): the row's pick of the wave's MACs
+            constexpr uint32_t PW = 64 / R;
+            const uint32_t row = rowbase4 / (4u * R);
+            uint32_t m0 = 0, m1 = 0, m2 = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) {
+                m0 = (row == i) ? wmac[3 * i] : m0;
+                m1 = (row == i) ? wmac[3 * i + 1] : m1;
+                m2 = (row == i) ? wmac[3 * i + 2] : m2;
+            }
+            h0.x = m0;
+            h0.y = m1;
+            h0.z = m2;
         }
         if (fwd && rl == 1) {  // ttl-- (279): byte 22 (dword 1) or 26 (dword 2), never borrows
             if (tagged) h0.z -= 1u << 16;
@@ -711,7 +716,9 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             }
         }
     };
-    if (FWD && fwd && !(DBG & 1)) {  // the rewritten header bytes, before the cold path reads them
+    // the rewritten header bytes, beside the checksum bytes (one write transaction per line;
+    // storing them before the sums measured 0.5% slower) and before the cold path reads them
+    if (FWD && fwd && !(DBG & 1)) {
         if (rl == 0) ((uint4*)frame)[0] = h0;  // frame len >= 34: chunk 0 is the frame's own
         if (rl == 1) frame[tagged ? 26 : 22] = (uint8_t)(ttl - 1u);
     }
@@ -778,24 +785,57 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     const uint32_t stride = gridDim.x * (BS / R);
     const uint64_t w0 = (uint64_t)blockIdx.x * (BS / R) + rfl(threadIdx.x >> 6) * PW;
     if (w0 >= n) return;
+    // Fused L3 forward: the wave's PW next-hop indexes and their table rows are wave-uniform.
+    // Read through the constant address space they are scalar loads on lgkmcnt, issued with the
+    // descriptors so both arrive in one round trip (as generic loads the compiler made each
+    // index a vector load drained by vmcnt(0) ahead of the frame loads: four serial memory
+    // round trips per wave).
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    auto load_nh = [&](uint32_t (&q)[PW], uint64_t pw) {
+        const cu32* nhp = (const cu32*)fa.nh + pw;
+        if (pw + PW <= n) {
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) q[i] = nhp[i];
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
+        }
+    };
     DescW<PW> Dn = load_descw<PW>(desc, w0, n);
+    uint32_t Qn[PW];
+    if (FWD && !(DBG & 16)) load_nh(Qn, w0);
+    if (FWD && (DBG & 16)) {  // measurement: next hop 0 for every packet, no index loads
+#pragma unroll
+        for (uint32_t i = 0; i < PW; ++i) Qn[i] = 0;
+    }
     for (uint64_t pw = w0; pw < n; pw += stride) {
         const DescW<PW> D = Dn;
-        if (pw + stride < n) Dn = load_descw<PW>(desc, pw + stride, n);  // prefetch (lgkmcnt)
+        uint32_t q[PW];
+#pragma unroll
+        for (uint32_t i = 0; i < PW; ++i) q[i] = FWD ? Qn[i] : 0u;
+        if (pw + stride < n) {  // prefetch (lgkmcnt)
+            Dn = load_descw<PW>(desc, pw + stride, n);
+            if (FWD && !(DBG & 16)) load_nh(Qn, pw + stride);
+        }
         RowStage<K> S;
         uint32_t nh = 0;
-        if (FWD) {  // the wave's PW next-hop indexes, scalar like the descriptors
-            uint32_t q[PW];
+        uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
+        if (FWD) {
 #pragma unroll
-            for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? fa.nh[pw + i] : NFCS_NH_NONE;
-#pragma unroll
-            for (uint32_t i = 0; i < PW; ++i) nh |= (row == i) ? q[i] : 0u;
+            for (uint32_t i = 0; i < PW; ++i) {
+                nh |= (row == i) ? q[i] : 0u;
+                const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i])
+                                                    : (const cu32*)&g_zero16;
+                wmac[3 * i] = m[0];
+                wmac[3 * i + 1] = m[1];
+                wmac[3 * i + 2] = m[2];
+            }
         }
         if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
         row_stage<K, NT, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
                                  rl, nh, &fa);
         if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n);
+        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac);
     }
 }
 
@@ -892,6 +932,22 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, BS>),                         \
                        dim3((n + (BS / 16) - 1) / (BS / 16)), dim3(BS), 0, stream, arena, arena_bytes, \
                        desc, n, base16, status, patch, nofwd)
+    // occupancy-bounded forms: update_rows_kernel<K, NT, R, DBG, OCC, FWD, SV, BS>
+    case 70: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 8, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8 waves per SIMD (64 VGPRs)
+    case 71: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 8, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // ... one-wave workgroups
+    case 72: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 7, false, 1, 256>), dim3(rows_grid(8)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8-lane rows K=6 at 7 waves per SIMD
+    case 73: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 7, false, 1, 64>),
+                                dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // ... one-wave workgroups
+    case 74: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 5, false, 1, 64>),
+                                dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 8-lane K=12, 5 waves per SIMD
     case 60: NFCS_ROWS_BS(64); break;    // default kernel, one wave per workgroup
     case 61: NFCS_ROWS_BS(128); break;
     case 62: NFCS_ROWS_BS(512); break;
@@ -960,14 +1016,29 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream, int grid) {
+                             hipStream_t stream, int grid, int variant) {
     (void)di;
     if (n == 0) return hipSuccess;
     const uint32_t need = (n + 15u) / 16u;
     const int g = grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
     const FwdArgs fa = {nh, table, table_n};
-    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, true, 1>), dim3(g), dim3(kBlock), 0, stream,
-                       arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa);
+#define NFCS_FWD(DBG, OCC, F)                                                                    \
+    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, DBG, OCC, F, 1>), dim3(g), dim3(kBlock), 0, \
+                       stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa)
+    switch (variant) {
+#ifdef NFCS_EXPERIMENTS
+    // ablations (measurement build only): results differ from the reference on purpose
+    case 101: NFCS_FWD(1, 7, true); break;   // no frame stores
+    case 102: NFCS_FWD(0, 7, false); break;  // the plain update, same launch
+    case 103: NFCS_FWD(0, 1, true); break;   // no occupancy bound: 81 VGPRs, 6 waves per SIMD
+    case 116: NFCS_FWD(16, 7, true); break;  // no next-hop index loads (next hop 0)
+
+#endif
+    // 7 waves per SIMD (72 VGPRs, no scratch; the compiler alone picks 81 VGPRs = 6 waves and
+    // the kernel runs 4-5% slower: variant 103)
+    default: NFCS_FWD(0, 7, true); break;
+    }
+#undef NFCS_FWD
     return hipGetLastError();
 }
 
