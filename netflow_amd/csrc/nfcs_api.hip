@@ -305,7 +305,7 @@ NFCS_API int nfcs_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u) || ((uintptr_t)d_keys & 15u))
         return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash,
-                                    pick(c, stream)));
+                                    pick(c, stream), c->variant));
     return NFCS_OK;
 }
 
@@ -551,7 +551,8 @@ NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uin
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
-        NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st));
+        NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st,
+                                        c->variant));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

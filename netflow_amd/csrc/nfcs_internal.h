@@ -69,7 +69,7 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,
-                            uint32_t* hashes, hipStream_t stream);
+                            uint32_t* hashes, hipStream_t stream, int variant = 0);
 
 hipError_t launch_gen_config(const DevInfo& di, int config, uint64_t seed, uint64_t first,
                              uint32_t n, uint8_t* arena, uint64_t arena_bytes,

@@ -1340,33 +1340,28 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
 // ---- flow-key extract + hash -----------------------------------------------
 // PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) on the first
 // 128 bytes of each frame: one 8-lane DPP row per packet (lane rl holds frame bytes
-// 16rl..16rl+15, one global_load_dwordx4), 8 packets per wave. Every field the key reads lies
-// below byte 82 (l2 18 + IHL 60 + 4 port bytes), so one slot covers it. Fields reach the row by
-// the same RowHdr broadcasts and 802.1Q view as the checksum plan; the record's 16 dwords are
-// stored by lanes 0-3 (64 contiguous bytes per packet, 512 per wave).
+// 16rl..16rl+15, one global_load_dwordx4). Every field the key reads lies below byte 82 (l2 18 +
+// IHL 60 + 4 port bytes), so one slot covers it. Fields reach the row by the same RowHdr
+// broadcasts and 802.1Q view as the checksum plan; the record's 16 dwords are stored by lanes
+// 0-3 (64 contiguous bytes per packet).
+//
+// The access pattern is one isolated 128-byte line per frame; MI355X serves those at ~46 G
+// lines/s at a 1536-byte stride (tools/stride_read.hip) when enough are in flight. A wave
+// therefore takes K slots of 8 packets (8K packets): lane l loads descriptor pw + l in one
+// coalesced load, each row picks its slot's descriptor with ds_bpermute, and all K header
+// lines are in flight before the first is parsed (session 2's one-slot form: 8 lines per wave,
+// 22.8 G lines/s).
 static_assert(sizeof(nfcs_flow_key) == 64, "nfcs_flow_key is a 64-byte record");
 
 DEV uint32_t be32x(uint32_t le) { return __builtin_bswap32(le); }
 
-__global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __restrict__ arena,
-                                                           uint64_t arena_bytes,
-                                                           const nfcs_desc* __restrict__ desc,
-                                                           uint32_t n, nfcs_flow_key* __restrict__ keys,
-                                                           uint32_t* __restrict__ hashes) {
+// One packet per 8-lane row: c0 = frame bytes 16rl..16rl+15 (zeros past len; len 0 when the
+// descriptor is out of bounds, which yields the all-zero record and hash of a dead packet).
+DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uint32_t rl,
+                      uint32_t rowbase4, nfcs_flow_key* __restrict__ keys,
+                      uint32_t* __restrict__ hashes) {
     constexpr int R = 8;
-    constexpr uint32_t PW = 64 / R;
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
-    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
-    if (pw >= n) return;
-    const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
-    const uint64_t p = pw + row;
-    const uint64_t off = (uint64_t)d.off16 * 16u;
-    const bool live = p < n && off + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes;
-    const uint32_t len = live ? d.len : 0u;
-    const uint4* src = (const uint4*)(arena + (live ? off : 0));
-    const uint4 c0 = ld16<0>((rl * 16u < len) ? src + rl : &g_zero16);
-
+    const bool live = len != 0;
     const RowHdr<R> h{c0, rowbase4};
     const bool eth = len >= 14;
     const uint32_t dw0 = h.dw(0), dw1 = h.dw(1), dw2 = h.dw(2);
@@ -1424,20 +1419,61 @@ __global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __rest
         } else {
             r = v6 ? make_uint4(d6[0], d6[1], d6[2], d6[3]) : make_uint4(d4, 0u, 0u, 0u);
         }
-        if (!live) r = make_uint4(0u, 0u, 0u, 0u);
         if (p < n) ((uint4*)(keys + p))[rl] = r;
     }
     if (hashes && rl == 0 && p < n) hashes[p] = hv;
 }
 
+template <int K>
+__global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __restrict__ arena,
+                                                           uint64_t arena_bytes,
+                                                           const nfcs_desc* __restrict__ desc,
+                                                           uint32_t n, nfcs_flow_key* __restrict__ keys,
+                                                           uint32_t* __restrict__ hashes) {
+    static_assert(K >= 1 && K <= 8, "slots of 8 packets per wave");
+    constexpr int R = 8;
+    constexpr uint32_t PR = 64 / R, PW = PR * K;  // rows per wave, packets per wave
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t pw = ((uint64_t)blockIdx.x * (kBlock / 64) + rfl(threadIdx.x >> 6)) * PW;
+    if (pw >= n) return;
+    uint2 dl = make_uint2(0u, 0u);  // lane l: descriptor of packet pw + l
+    if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
+    uint4 c[K];
+    uint32_t L[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t sl = (uint32_t)k * PR + row;  // slot k, this row: packet pw + sl
+        const uint32_t off16 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.x);
+        const uint32_t dlen = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.y);
+        const uint64_t off = (uint64_t)off16 * 16u;
+        const bool live = pw + sl < n && off + (((uint64_t)dlen + 15u) & ~15ull) <= arena_bytes;
+        L[k] = live ? dlen : 0u;
+        const uint4* src = (const uint4*)(arena + (live ? off : 0));
+        c[k] = ld16<0>((rl * 16u < L[k]) ? src + rl : &g_zero16);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        flow_key_row(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
+}
+
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,
-                            uint32_t* hashes, hipStream_t stream) {
+                            uint32_t* hashes, hipStream_t stream, int variant) {
     (void)di;
     if (n == 0) return hipSuccess;
-    const uint32_t blocks = (n + 31u) / 32u;  // 8 rows per wave, 4 waves per workgroup
-    hipLaunchKernelGGL(flow_keys_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, arena_bytes,
-                       desc, n, keys, hashes);
+#define NFCS_FK(K)                                                                                \
+    hipLaunchKernelGGL((flow_keys_kernel<K>), dim3((n + 32u * K - 1u) / (32u * K)), dim3(kBlock), \
+                       0, stream, arena, arena_bytes, desc, n, keys, hashes)
+    switch (variant) {
+#ifdef NFCS_EXPERIMENTS
+    case 81: NFCS_FK(1); break;  // session 2: one slot, 8 packets per wave
+    case 82: NFCS_FK(2); break;
+    case 88: NFCS_FK(8); break;
+#endif
+    default: NFCS_FK(4); break;  // 32 packets per wave
+    }
+#undef NFCS_FK
     return hipGetLastError();
 }
 
