@@ -495,6 +495,21 @@ NFCS_API int nfcs_stream_sync(nfcs_ctx* c, void* stream) {
     return NFCS_OK;
 }
 
+#ifdef NFCS_EXPERIMENTS
+// Measurement build only: one launch of a timeline variant (90-93) with 8 u64 per wave of
+// 16-lane rows written to d_ts (tools/wave_timeline.py).
+NFCS_API int nfcs_exp_wave_timeline(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
+                                    const nfcs_desc* d_desc, uint32_t n, int variant,
+                                    uint64_t* d_ts) {
+    if (!c || !d_ts || variant < 90 || variant > 93) return NFCS_EINVAL;
+    hipStream_t st = pick(c, nullptr);
+    NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, nullptr,
+                                 (nfcs_patch*)d_ts, st, variant, c->grid, c->work(n)));
+    NFCS_HIP(hipStreamSynchronize(st));
+    return NFCS_OK;
+}
+#endif
+
 NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms) {

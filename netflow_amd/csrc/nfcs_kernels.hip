@@ -564,9 +564,24 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 
 // DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
 // (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
+// Measurement builds (DBG 256): per-wave timeline. s_memtime returns the shader clock; the
+// trailing lgkmcnt(0) makes the stamp wait for every scalar load issued before it.
+DEV uint64_t ts_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
 template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false, int SV = 0>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
-                     nfcs_patch* patch, uint32_t table_n = 0, const uint32_t* wmac = nullptr) {
+                     nfcs_patch* patch, uint32_t table_n = 0, const uint32_t* wmac = nullptr,
+                     uint64_t* T = nullptr) {
+    if (DBG & 256) {  // the header slot (first of the K loads) has landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K - 1) : "memory");
+        T[2] = ts_now();
+    }
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
@@ -679,6 +694,10 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             if (tailfix) acc += 255u * ((comp(lc, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
         }
     }
+    if (DBG & 256) {  // every slot has landed and been summed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        T[3] = ts_now();
+    }
     // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t cmax = wave_max_rows<R>(nre);
     for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
@@ -722,7 +741,15 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         if (rl == 0) ((uint4*)frame)[0] = h0;  // frame len >= 34: chunk 0 is the frame's own
         if (rl == 1) frame[tagged ? 26 : 22] = (uint8_t)(ttl - 1u);
     }
-    emit(S.valid && !slow, st, ipw, l4w, true);
+    emit(S.valid && !slow && !(DBG & 256), st, ipw, l4w, true);
+    if (DBG & 256) {  // frame stores issued; status / patch are not written in this mode
+        if (!(DBG & 1) && S.valid && !slow && rl < 4) {
+            const uint32_t w = (rl & 2u) ? l4w : ipw;
+            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+        }
+        T[4] = ts_now();
+    }
     if (DBG & 4) __builtin_amdgcn_s_setprio(0);
     if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
         // Uncommon headers, handled last so that only the frame address and length are live
@@ -801,7 +828,28 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
             for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
         }
     };
+    // measurement (DBG 64 / 128): touch the descriptor line of the wave that starts ~one
+    // residency later, so its scalar descriptor load hits L2 instead of HBM
+    uint32_t pf = 0;
+    if (DBG & 192) {
+        constexpr uint64_t D = (DBG & 64) ? 16384u : 65536u;  // packets ahead
+        uint32_t z = 0;
+        asm volatile("" : "+v"(z));  // a vector load (a scalar one would be waited on at once)
+        if (lane == 0 && w0 + D < n) pf = ((const uint32_t*)(desc + w0 + D))[z];
+    }
+    uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (DBG & 256) {
+        uint64_t rt;
+        uint32_t hw, xcc;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        T[0] = ts_now();
+        T[6] = rt;
+        T[7] = ((uint64_t)xcc << 32) | hw;
+    }
     DescW<PW> Dn = load_descw<PW>(desc, w0, n);
+    if (DBG & 256) T[1] = ts_now();  // the wave's descriptors have landed
     uint32_t Qn[PW];
     if (FWD && !(DBG & 16)) load_nh(Qn, w0);
     if (FWD && (DBG & 16)) {  // measurement: next hop 0 for every packet, no index loads
@@ -835,7 +883,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
         row_stage<K, NT, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
                                  rl, nh, &fa);
         if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac);
+        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac, T);
+    }
+    if (DBG & 192) asm volatile("" ::"v"(pf));  // keeps the prefetch load
+    if (DBG & 256) {  // the frame stores acknowledged; the wave's stamps go to `patch`
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        T[5] = ts_now();
+        if (lane < 8) {
+            uint64_t t = T[0];
+#pragma unroll
+            for (uint32_t i = 1; i < 8; ++i) t = (lane == i) ? T[i] : t;
+            ((uint64_t*)patch)[(w0 / PW) * 8u + lane] = t;
+        }
     }
 }
 
@@ -900,8 +959,10 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                                 dim3(kBlock), di.lds_pad, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;
     case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
-    case 29:  // as 0 in one-wave workgroups (4 packets each): measured +2-3% on C3, -0.7% on C1
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, 64>), dim3((n + 3u) / 4u),
+    case 29:  // as 0 in one-wave workgroups (4 packets each): measured +2-3% on C3, -0.7% on C1;
+              // __launch_bounds__ 7 waves/SIMD caps the kernel at 94 SGPRs: at the compiler's 106
+              // the SGPR file (800 per SIMD, 16-register granule + 16) admits only 6 (C3 +2%)
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 64>), dim3((n + 3u) / 4u),
                            dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
                            nofwd);
         break;
@@ -945,9 +1006,47 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 73: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 7, false, 1, 64>),
                                 dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                 base16, status, patch, nofwd); break;  // ... one-wave workgroups
+    case 75: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // default held at 7 waves/SIMD (SGPRs <= 96)
+    case 76: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 64>),
+                                dim3(grid > 0 && (uint32_t)grid < (n + 3u) / 4u ? (uint32_t)grid : (n + 3u) / 4u),
+                                dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
+                                nofwd); break;  // 29 with a grid-stride loop when NFCS_GRID is set
+    case 77: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 76 + descriptor prefetch 16k ahead
+    case 78: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // ... 64k ahead
     case 74: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 5, false, 1, 64>),
                                 dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                 base16, status, patch, nofwd); break;  // 8-lane K=12, 5 waves per SIMD
+    case 64: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // descriptor prefetch 16k packets ahead
+    case 65: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // ... 64k packets ahead
+    case 66: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 1, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 16k ahead, one-wave groups
+    case 67: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 1, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 64k ahead, one-wave groups
+    // per-wave timeline (tools/wave_timeline.py): `patch` = 8 u64 per wave
+    case 90: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 256, 7, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;
+    case 91: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 256, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;
+    case 92: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 257, 7, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // ... no frame stores
+    case 93: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 257, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;
     case 60: NFCS_ROWS_BS(64); break;    // default kernel, one wave per workgroup
     case 61: NFCS_ROWS_BS(128); break;
     case 62: NFCS_ROWS_BS(512); break;
@@ -1034,8 +1133,8 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     case 116: NFCS_FWD(16, 7, true); break;  // no next-hop index loads (next hop 0)
 
 #endif
-    // 7 waves per SIMD (72 VGPRs, no scratch; the compiler alone picks 81 VGPRs = 6 waves and
-    // the kernel runs 4-5% slower: variant 103)
+    // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
+    // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower: variant 103)
     default: NFCS_FWD(0, 7, true); break;
     }
 #undef NFCS_FWD

@@ -99,6 +99,18 @@ def test_gpu_flow_fresh_and_bad_desc(engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 7, 9, 31, 33, 127, 129, 1001])
+def test_gpu_flow_ragged_counts(engine, n):
+    # a wave takes 32 packets (4 slots of 8 rows): counts that end mid-slot and mid-wave
+    frames = oracle.fuzz_frames(43, 0, n)
+    arena, desc = oracle.pack_frames(frames)
+    rrecs, rh = oracle.flow_keys_batch(arena, desc)
+    recs, hashes = run_flow(engine, arena, desc)
+    assert np.array_equal(hashes, rh)
+    assert np.array_equal(recs, rrecs)
+
+
+@pytest.mark.gpu
 def test_gpu_flow_config_batch(engine):
     n = 1 << 16
     d_arena, nbytes, d_desc, hdesc = engine.config_batch(3, 20250620, 0, n, 128)
