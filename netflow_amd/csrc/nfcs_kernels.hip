@@ -958,7 +958,6 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 24: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1>), dim3(rows_grid(16)),
                                 dim3(kBlock), di.lds_pad, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;
-    case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
     case 29:  // as 0 in one-wave workgroups (4 packets each): measured +2-3% on C3, -0.7% on C1;
               // __launch_bounds__ 7 waves/SIMD caps the kernel at 94 SGPRs: at the compiler's 106
               // the SGPR file (800 per SIMD, 16-register granule + 16) admits only 6 (C3 +2%)
@@ -966,16 +965,6 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                            dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
                            nofwd);
         break;
-    case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
-    case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
-    case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
-    case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
-    case 25: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8-lane rows K=6, branch-free sums
-    case 26: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8-lane rows K=12, branch-free sums
     case 8: {  // split: checksum pass without frame stores, then the patch pass
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
@@ -989,6 +978,17 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         break;
     }
 #ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
+    case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
+    case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
+    case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
+    case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
+    case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
+    case 25: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8-lane rows K=6, branch-free sums
+    case 26: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 8-lane rows K=12, branch-free sums
 #define NFCS_ROWS_BS(BS)                                                                          \
     hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, BS>),                         \
                        dim3((n + (BS / 16) - 1) / (BS / 16)), dim3(BS), 0, stream, arena, arena_bytes, \
