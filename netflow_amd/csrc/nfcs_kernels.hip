@@ -49,6 +49,18 @@ DEV uint32_t comp(const uint4& v, uint32_t j) {
 }
 
 
+DEV uint4 put_byte(const uint4& v, uint32_t i, uint32_t b) {
+    uint32_t r[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t sh = 8u * (i & 3u);
+        const uint32_t m = ((i >> 2) == j) ? (0xFFu << sh) : 0u;
+        r[j] = (comp(v, j) & ~m) | ((b << sh) & m);
+    }
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+
 // ---- exact sequential path (IHL < 5 overlap cases), one lane --------------------------------
 // Mirrors packet.hpp:722-890 byte by byte on global memory, in the reference's write order.
 struct SeqOut { uint32_t st, ip_off, ip_val, l4_off, l4_val; };
@@ -473,6 +485,29 @@ DEV uint4 ld16(const uint4* p) {
     return *p;
 }
 
+// Frame stores. WT: write-through at agent scope (`sc1`): the L2 keeps no dirty copy of the
+// frame's line, so the line leaves as a clean eviction and the write goes to memory at once
+// instead of as a later write-back in the middle of the read stream (session 3: C1 +2.5%,
+// C3 +5% over plain stores; `sc0 sc1` measured the same, `sc0 sc1 nt` 5% worse).
+template <bool WT>
+DEV void st8(uint8_t* p, uint32_t b) {
+    if (WT) __hip_atomic_store(p, (uint8_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = (uint8_t)b;
+}
+template <bool WT>
+DEV void st16(uint4* p, const uint4& v) {
+    if (WT) {
+        // One dwordx4 sc1 store. The s_nop covers the gfx9 hazard of a VALU write to the data
+        // VGPRs of a store wider than 8 bytes right after it, which hipcc's hazard recognizer
+        // does not see inside inline asm (without it the VLAN kernel stored clobbered dwords).
+        // Two 8-byte atomic sc1 stores instead cost 37% on VLAN C1.
+        const u32x4_t t = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
+    } else {
+        *p = v;
+    }
+}
+
 // Descriptors of the wave's four rows: packets w, w+1, w+2, w+3 are consecutive in the
 // descriptor array, so one wave-uniform scalar load (s_load_dwordx8) fetches all four; each
 // lane picks its row's pair. Counted on lgkmcnt, so prefetching them never holds up a vmcnt
@@ -723,7 +758,19 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         if (!(DBG & 1) && frame_stores && on && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w_ : ipw_;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) {
+                const uint8_t b = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+                // measurement builds: 512 nt, 1024 system scope (sc0 sc1), 4096 sc0 sc1 nt,
+                // 8192 plain (write-back) stores; default write-through (sc1)
+                if (DBG & 512) __builtin_nontemporal_store(b, frame + pos);
+                else if (DBG & 1024) __hip_atomic_store(frame + pos, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else if (DBG & 4096) {
+                    const uint32_t bv = b;
+                    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(frame + pos), "v"(bv) : "memory");
+                } else {
+                    st8<!(DBG & 8192)>(frame + pos, b);
+                }
+            }
         }
         if (on && rl == 0) {
             if (status) status[S.p] = (uint8_t)st_;
@@ -735,18 +782,46 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             }
         }
     };
-    // the rewritten header bytes, beside the checksum bytes (one write transaction per line;
-    // storing them before the sums measured 0.5% slower) and before the cold path reads them
-    if (FWD && fwd && !(DBG & 1)) {
-        if (rl == 0) ((uint4*)frame)[0] = h0;  // frame len >= 34: chunk 0 is the frame's own
-        if (rl == 1) frame[tagged ? 26 : 22] = (uint8_t)(ttl - 1u);
+    // Segment stores (the fused forward; DBG 16384 for the plain update, measured no faster
+    // there): one write-through segment per packet. Lanes 0..c store chunks 0..c of the header
+    // (c = the last chunk holding a byte to write) from the header registers with the checksum
+    // bytes and the forward's rewrite patched in; unchanged bytes are rewritten with the values
+    // just read from them (a frame never shares a 16-byte chunk with another frame). L3 forward
+    // +1.5% over a 16-byte store + byte stores (variant 119).
+    constexpr bool SEG = (FWD && !(DBG & 32768)) || (DBG & 16384);
+    if (SEG) {
+        if (!(DBG & 1) && S.valid && !slow) {
+            uint4 v = h0;
+            uint32_t last = (FWD && fwd) ? 1u : 0u;
+            bool any = FWD && fwd;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t w = (t < 2) ? ipw : l4w;
+                const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
+                if ((w & 0xFFFFu) != NFCS_PATCH_NONE) {
+                    any = true;
+                    last = max(last, pos >> 4);
+                    if ((pos >> 4) == rl) v = put_byte(v, pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
+                }
+            }
+            if (any && rl <= last) st16<true>((uint4*)frame + rl, v);
+        }
+        emit(S.valid && !slow, st, ipw, l4w, false);
+    } else {
+        // the rewritten header bytes, beside the checksum bytes (one write transaction per
+        // line; storing them before the sums measured 0.5% slower) and before the cold path
+        // reads them
+        if (FWD && fwd && !(DBG & 1)) {
+            if (rl == 0) st16<!(DBG & 8192)>((uint4*)frame, h0);  // len >= 34: chunk 0 is the frame's own
+            if (rl == 1) st8<!(DBG & 8192)>(frame + (tagged ? 26 : 22), ttl - 1u);
+        }
+        emit(S.valid && !slow && !(DBG & 256), st, ipw, l4w, true);
     }
-    emit(S.valid && !slow && !(DBG & 256), st, ipw, l4w, true);
     if (DBG & 256) {  // frame stores issued; status / patch are not written in this mode
         if (!(DBG & 1) && S.valid && !slow && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w : ipw;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<!(DBG & 8192)>(frame + pos, w >> (16 + 8 * (rl & 1u)));
         }
         T[4] = ts_now();
     }
@@ -756,6 +831,28 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
         // exact sequential emulation, which writes its own bytes) and the region is re-summed
         // from memory.
+        if (FWD && SEG && !(DBG & 1) && slow && fwd) {
+            // segment stores skip uncommon headers: their forward rewrite goes out here, from
+            // the next-hop MACs (SGPRs) and the TTL byte in memory (the header registers are
+            // dead by now, which keeps the fast path free of spills)
+            if (rl == 0) {
+                constexpr uint32_t PW = 64 / R;
+                const uint32_t row = rowbase4 / (4u * R);
+                uint32_t m[3] = {0, 0, 0};
+#pragma unroll
+                for (uint32_t i = 0; i < PW; ++i) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 3; ++j) m[j] = (row == i) ? wmac[3 * i + j] : m[j];
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 3; ++j)
+                    __hip_atomic_store((uint32_t*)frame + j, m[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (rl == 1) {
+                const uint32_t o = tagged ? 26u : 22u;
+                st8<true>(frame + o, frame[o] - 1u);
+            }
+        }
         if (FWD) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // see the header stores
         RPlan Q = rplan_none(0);
         SeqOut o = {0, 0, 0, 0, 0};
@@ -901,6 +998,7 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
 // Split mode, second pass: write the patch records of the checksum pass into the frames. A
 // write-only pass over 8 bytes per packet, so the frame stream of the first pass carries no
 // scattered stores (each write transaction in a read stream costs far more than its bytes).
+template <bool WT>
 __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restrict__ arena,
                                                                const nfcs_desc* __restrict__ desc,
                                                                uint32_t n, uint32_t base16,
@@ -911,12 +1009,17 @@ __global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restri
         if (ipo == NFCS_PATCH_NONE && l4o == NFCS_PATCH_NONE) continue;
         uint8_t* f = arena + ((uint64_t)desc[i].off16 - base16) * 16u;
         if (ipo != NFCS_PATCH_NONE) {  // l2 + 10: always even
-            *(uint16_t*)(f + ipo) = (uint16_t)(r.y & 0xFFFFu);
+            if (WT) __hip_atomic_store((uint16_t*)(f + ipo), (uint16_t)(r.y & 0xFFFFu), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            else *(uint16_t*)(f + ipo) = (uint16_t)(r.y & 0xFFFFu);
         }
         if (l4o != NFCS_PATCH_NONE) {  // TCP's field at l4 + 15 is odd
             if (l4o & 1u) {
-                f[l4o] = (uint8_t)(r.y >> 16);
-                f[l4o + 1] = (uint8_t)(r.y >> 24);
+                st8<WT>(f + l4o, r.y >> 16);
+                st8<WT>(f + l4o + 1, r.y >> 24);
+            } else if (WT) {
+                __hip_atomic_store((uint16_t*)(f + l4o), (uint16_t)(r.y >> 16), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 *(uint16_t*)(f + l4o) = (uint16_t)(r.y >> 16);
             }
@@ -965,7 +1068,8 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                            dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
                            nofwd);
         break;
-    case 8: {  // split: checksum pass without frame stores, then the patch pass
+    case 8: {  // split: checksum pass without frame stores, then the patch pass (plain stores:
+               // a write-through patch pass measured C2 0.805 vs 0.823, variant 9)
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
         hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
@@ -973,7 +1077,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                            nofwd);
         int ga = (int)((n + kBlock - 1) / kBlock);
         if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
                            base16, pp);
         break;
     }
@@ -1013,6 +1117,45 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                                 dim3(grid > 0 && (uint32_t)grid < (n + 3u) / 4u ? (uint32_t)grid : (n + 3u) / 4u),
                                 dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
                                 nofwd); break;  // 29 with a grid-stride loop when NFCS_GRID is set
+    case 79: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 512, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // default with non-temporal checksum stores
+    case 80: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // ... system-scope (write-through) stores
+    case 84: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // plain (write-back) checksum stores, sessions 1-2
+    case 83: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 29 with plain stores
+    case 9: {  // split mode with a write-through patch pass
+        nfcs_patch* pp = patch ? patch : ws;
+        if (!pp) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
+                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
+                           nofwd);
+        int ga = (int)((n + kBlock - 1) / kBlock);
+        if (ga > di.cus * 8) ga = di.cus * 8;
+        hipLaunchKernelGGL(apply_patches_kernel<true>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+                           base16, pp);
+        break;
+    }
+    case 85: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 4096, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // ... sc0 sc1 nt
+    case 86: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // 29 with system-scope stores
+    case 87: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // 80 at 7 waves/SIMD
+    case 94: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // one write-through segment store per packet
+    case 95: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // ... in the short-frame form
     case 77: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 7, false, 1, 64>),
                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                 base16, status, patch, nofwd); break;  // 76 + descriptor prefetch 16k ahead
@@ -1086,7 +1229,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         else NFCS_LP(6, 8, 1, pp);
         int ga = (int)((n + kBlock - 1) / kBlock);
         if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
                            base16, pp);
         break;
     }
@@ -1131,6 +1274,8 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     case 102: NFCS_FWD(0, 7, false); break;  // the plain update, same launch
     case 103: NFCS_FWD(0, 1, true); break;   // no occupancy bound: 81 VGPRs, 6 waves per SIMD
     case 116: NFCS_FWD(16, 7, true); break;  // no next-hop index loads (next hop 0)
+    case 118: NFCS_FWD(8192 | 32768, 7, true); break;  // plain (write-back) 16-B + byte stores
+    case 119: NFCS_FWD(32768, 7, true); break;         // write-through 16-B + byte stores
 
 #endif
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
@@ -1175,16 +1320,6 @@ DEV uint4 keep_tail(const uint4& nv, const uint4& ov, uint32_t o, uint32_t wend)
 }
 
 // Byte i (0..15) of a chunk register := b.
-DEV uint4 put_byte(const uint4& v, uint32_t i, uint32_t b) {
-    uint32_t r[4];
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t sh = 8u * (i & 3u);
-        const uint32_t m = ((i >> 2) == j) ? (0xFFu << sh) : 0u;
-        r[j] = (comp(v, j) & ~m) | ((b << sh) & m);
-    }
-    return make_uint4(r[0], r[1], r[2], r[3]);
-}
 
 DEV uint32_t dpp_prev(uint32_t x) {  // lane rl gets lane rl-1 of its row (0 for rl = 0)
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xF, 0xF, true);
@@ -1222,7 +1357,7 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K, int K2 = 2>
+template <int K, int K2 = 2, bool WT = false>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1334,13 +1469,13 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst || (k == 0 && patched)) ((uint4*)frame)[c] = nv[k];
+            if (c < nst || (k == 0 && patched)) st16<WT>((uint4*)frame + c, nv[k]);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst) ((uint4*)frame)[c] = nv[k];
+            if (c < nst) st16<WT>((uint4*)frame + c, nv[k]);
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
         // the rest of a long frame in batches of K2 slots (K2 < K saves VGPRs: w and e live
@@ -1360,7 +1495,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
-                if (c < nst) ((uint4*)frame)[c] = e[k];
+                if (c < nst) st16<WT>((uint4*)frame + c, e[k]);
             }
         }
         l4w = finish(acc);
@@ -1370,7 +1505,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             const uint32_t w = (t < 2) ? ipw : l4w;
             const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
             if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl)
-                frame[pos] = (uint8_t)(w >> (16 + 8 * (t & 1u)));
+                st8<WT>(frame + pos, w >> (16 + 8 * (t & 1u)));
         }
     }
     const uint32_t st0 = bad ? (uint32_t)NFCS_ST_BAD_DESC
@@ -1412,7 +1547,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
         if (slow && !seq && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w2 : ipw2;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) frame[pos] = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<WT>(frame + pos, w >> (16 + 8 * (rl & 1u)));
         }
         if (slow && rl == 0 && status)
             status[p] = (uint8_t)((seq ? (ost | NFCS_ST_FLAG_OVERLAP) : Q.st) | NFCS_ST_FLAG_VLAN);
@@ -1428,11 +1563,16 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
     // (variant 31: 94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, and capping the
     // occupancy lower with LDS padding slower still (profiles/r01_s2_occupancy.md).
     if (variant == 31)
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 2>), dim3(blocks), dim3(kBlock), di.lds_pad, stream, arena,
-                           arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
-    else
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6>), dim3(blocks), dim3(kBlock), di.lds_pad, stream, arena,
-                           arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 2, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
+                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+#ifdef NFCS_EXPERIMENTS
+    else if (variant == 32)  // plain (write-back) frame stores, sessions 1-2
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, false>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
+                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+#endif
+    else  // write-through (sc1) frame stores: +1.2% on C1 push/pop over plain stores
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
+                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     return hipGetLastError();
 }
 
