@@ -1596,6 +1596,7 @@ DEV uint32_t be32x(uint32_t le) { return __builtin_bswap32(le); }
 
 // One packet per 8-lane row: c0 = frame bytes 16rl..16rl+15 (zeros past len; len 0 when the
 // descriptor is out of bounds, which yields the all-zero record and hash of a dead packet).
+template <int ST = 0>  // record stores: 0 plain, 1 nt, 2 write-through (sc1), measurement
 DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uint32_t rl,
                       uint32_t rowbase4, nfcs_flow_key* __restrict__ keys,
                       uint32_t* __restrict__ hashes) {
@@ -1658,12 +1659,17 @@ DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uin
         } else {
             r = v6 ? make_uint4(d6[0], d6[1], d6[2], d6[3]) : make_uint4(d4, 0u, 0u, 0u);
         }
-        if (p < n) ((uint4*)(keys + p))[rl] = r;
+        if (p < n) {
+            uint4* q = (uint4*)(keys + p) + rl;
+            if (ST == 1) __builtin_nontemporal_store(u32x4_t{r.x, r.y, r.z, r.w}, (u32x4_t*)q);
+            else if (ST == 2) st16<true>(q, r);
+            else *q = r;
+        }
     }
     if (hashes && rl == 0 && p < n) hashes[p] = hv;
 }
 
-template <int K>
+template <int K, int ST = 1, int LD = 0>
 __global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            const nfcs_desc* __restrict__ desc,
@@ -1689,11 +1695,11 @@ __global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __rest
         const bool live = pw + sl < n && off + (((uint64_t)dlen + 15u) & ~15ull) <= arena_bytes;
         L[k] = live ? dlen : 0u;
         const uint4* src = (const uint4*)(arena + (live ? off : 0));
-        c[k] = ld16<0>((rl * 16u < L[k]) ? src + rl : &g_zero16);
+        c[k] = ld16<LD>((rl * 16u < L[k]) ? src + rl : &g_zero16);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        flow_key_row(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
+        flow_key_row<ST>(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
 }
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
@@ -1701,16 +1707,19 @@ hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t ar
                             uint32_t* hashes, hipStream_t stream, int variant) {
     (void)di;
     if (n == 0) return hipSuccess;
-#define NFCS_FK(K)                                                                                \
-    hipLaunchKernelGGL((flow_keys_kernel<K>), dim3((n + 32u * K - 1u) / (32u * K)), dim3(kBlock), \
+#define NFCS_FK(K, ST, LD)                                                                        \
+    hipLaunchKernelGGL((flow_keys_kernel<K, ST, LD>), dim3((n + 32u * K - 1u) / (32u * K)), dim3(kBlock), \
                        0, stream, arena, arena_bytes, desc, n, keys, hashes)
     switch (variant) {
 #ifdef NFCS_EXPERIMENTS
-    case 81: NFCS_FK(1); break;  // session 2: one slot, 8 packets per wave
-    case 82: NFCS_FK(2); break;
-    case 88: NFCS_FK(8); break;
+    case 81: NFCS_FK(1, 0, 0); break;  // session 2: one slot, 8 packets per wave, plain stores
+    case 82: NFCS_FK(2, 0, 0); break;
+    case 88: NFCS_FK(8, 0, 0); break;
+    case 84: NFCS_FK(4, 0, 0); break;  // plain record stores (nt: C1 +1.5-2%)
+    case 85: NFCS_FK(4, 2, 0); break;  // write-through record stores
+    case 86: NFCS_FK(4, 1, 1); break;  // ... and non-temporal header loads
 #endif
-    default: NFCS_FK(4); break;  // 32 packets per wave
+    default: NFCS_FK(4, 1, 0); break;  // 32 packets per wave, non-temporal record stores
     }
 #undef NFCS_FK
     return hipGetLastError();
