@@ -489,6 +489,10 @@ DEV uint4 ld16(const uint4* p) {
 // frame's line, so the line leaves as a clean eviction and the write goes to memory at once
 // instead of as a later write-back in the middle of the read stream (session 3: C1 +2.5%,
 // C3 +5% over plain stores; `sc0 sc1` measured the same, `sc0 sc1 nt` 5% worse).
+DEV void st16_nt(uint4* p, const uint4& v) {
+    __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)p);
+}
+
 template <bool WT>
 DEV void st8(uint8_t* p, uint32_t b) {
     if (WT) __hip_atomic_store(p, (uint8_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1150,6 +1154,15 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 87: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // 80 at 7 waves/SIMD
+    case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // every slot non-temporal (header too)
+    case 97: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 7, false, 1, 64>),
+                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // ... short-frame form
+    case 98: hipLaunchKernelGGL((update_rows_kernel<6, 0, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
+                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                                patch, nofwd); break;  // every slot default policy
     case 94: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384, 1, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // one write-through segment store per packet
@@ -1357,7 +1370,7 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K, int K2 = 2, bool WT = false>
+template <int K, int K2 = 2, bool WT = false, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1469,13 +1482,13 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst || (k == 0 && patched)) st16<WT>((uint4*)frame + c, nv[k]);
+            if (c < nst || (k == 0 && patched)) (NTS ? st16_nt((uint4*)frame + c, nv[k]) : st16<WT>((uint4*)frame + c, nv[k]));
         }
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst) st16<WT>((uint4*)frame + c, nv[k]);
+            if (c < nst) (NTS ? st16_nt((uint4*)frame + c, nv[k]) : st16<WT>((uint4*)frame + c, nv[k]));
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
         // the rest of a long frame in batches of K2 slots (K2 < K saves VGPRs: w and e live
@@ -1495,7 +1508,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
-                if (c < nst) st16<WT>((uint4*)frame + c, e[k]);
+                if (c < nst) (NTS ? st16_nt((uint4*)frame + c, e[k]) : st16<WT>((uint4*)frame + c, e[k]));
             }
         }
         l4w = finish(acc);
@@ -1566,6 +1579,9 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((vlan_rows_kernel<6, 2, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
                            arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
 #ifdef NFCS_EXPERIMENTS
+    else if (variant == 33)  // non-temporal chunk stores (checksum bytes written through)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, true>), dim3(blocks), dim3(kBlock), di.lds_pad,
+                           stream, arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     else if (variant == 32)  // plain (write-back) frame stores, sessions 1-2
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, false>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
                            arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
