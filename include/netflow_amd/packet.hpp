@@ -12,7 +12,13 @@
 // checksum bytes into each PacketBuffer in place — bit-exact with the reference; and
 // Packet::push_vlan / pop_vlan (packet.hpp:655-720) with their batched form
 //   netflow_amd::vlan_batch(Packet* const*, const uint32_t* ops, size_t, bool* ok)
-// (nfcs_vlan_device: tag insert / strip / re-tag and the checksums in one pass).
+// (nfcs_vlan_device: tag insert / strip / re-tag and the checksums in one pass); the switch's
+// transit-IPv4 forward (switch.hpp:247-294) for a burst
+//   netflow_amd::l3_forward_batch(Packet* const*, const uint32_t* next_hop, size_t, table, ...)
+// (nfcs_l3_forward_device: TTL--, MAC rewrite and the checksums in one pass); and
+// PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) for a burst
+//   netflow_amd::flow_keys_batch(Packet* const*, size_t, nfcs_flow_key*, uint32_t* hashes)
+// (nfcs_flow_keys_device: 64-byte FlowKey records in host order + hash_flow values).
 //
 // All checksum arithmetic happens on the GPU; there is no CPU fallback. Constructing the
 // engine without a gfx950 device throws std::runtime_error ("fail loudly").
@@ -137,9 +143,37 @@ public:
     inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
                           uint8_t* status = nullptr);
 
+    // Batched data path of the switch's transit-IPv4 forward (switch.hpp:247-294): for packet i
+    // with an IPv4 header, TTL <= 1 -> NFCS_ST_TTL_EXPIRED and next_hop[i] >= table_n ->
+    // NFCS_ST_NO_ROUTE (frame untouched, as the switch drops or punts it); otherwise TTL--,
+    // dst/src MAC = table[next_hop[i]] and update_checksums(), status | NFCS_ST_FLAG_FWD. The
+    // route and ARP lookups stay with the caller (next_hop indexes; NFCS_NH_NONE = no route).
+    inline int l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
+                                const nfcs_nexthop* table, uint32_t table_n,
+                                uint8_t* status = nullptr);
+
+    // PacketClassifier::extract_flow_key(pkt) and hash_flow(key) (packet_classifier.cpp:12-108)
+    // for a batch: keys[i] (optional) = the FlowKey fields in host order (nfcs_flow_key, with
+    // the hash in .hash), hashes[i] (optional) = hash_flow(key).
+    inline int flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
+                               uint32_t* hashes = nullptr);
+
     nfcs_ctx* ctx() const { return ctx_; }
 
 private:
+    // A device buffer for one call (next-hop tables, flow-key records).
+    struct DevTmp {
+        nfcs_ctx* c;
+        void* p = nullptr;
+        DevTmp(nfcs_ctx* c_, size_t bytes, int& rc) : c(c_) {
+            if (!rc) rc = nfcs_device_alloc(c, bytes ? bytes : 16, &p);
+        }
+        ~DevTmp() { if (p) nfcs_device_free(c, p); }
+    };
+    // Gather each packet's first min(len, limit) bytes (limit 0: all) into 16-byte aligned
+    // slots of the pinned arena; returns the arena bytes used.
+    size_t gather(Packet* const* pkts, size_t n, size_t limit);
+
     void release() {
         if (h_arena_) nfcs_host_free(ctx_, h_arena_);
         if (h_desc_) nfcs_host_free(ctx_, h_desc_);
@@ -348,6 +382,94 @@ inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, 
     return NFCS_OK;
 }
 
+inline size_t ChecksumEngine::gather(Packet* const* pkts, size_t n, size_t limit) {
+    uint8_t* arena = static_cast<uint8_t*>(h_arena_);
+    nfcs_desc* desc = static_cast<nfcs_desc*>(h_desc_);
+    size_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        size_t len = b ? b->get_data_length() : 0;
+        if (limit && len > limit) len = limit;
+        if (len) std::memcpy(arena + off, b->get_data_start_ptr(), len);
+        std::memset(arena + off + len, 0, ((len + 15) & ~size_t(15)) - len);
+        desc[i] = nfcs_desc{static_cast<uint32_t>(off >> 4), static_cast<uint32_t>(len)};
+        off += (len + 15) & ~size_t(15);
+    }
+    return off;
+}
+
+inline int ChecksumEngine::l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
+                                            const nfcs_nexthop* table, uint32_t table_n,
+                                            uint8_t* status) {
+    if (n == 0) return NFCS_OK;
+    if (!pkts || !next_hop || (table_n && !table) || n > 0xFFFFFFFFu) return NFCS_EINVAL;
+    std::lock_guard<std::mutex> lock(mu_);
+    size_t bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        bytes += ((b ? b->get_data_length() : 0) + 15) & ~size_t(15);
+    }
+    if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
+    int rc = reserve(bytes + 16, n);
+    if (rc) return rc;
+    const size_t off = gather(pkts, n, 0);
+    uint8_t* arena = static_cast<uint8_t*>(h_arena_);
+    const nfcs_desc* desc = static_cast<const nfcs_desc*>(h_desc_);
+    uint32_t* hnh = static_cast<uint32_t*>(h_ops_);
+    for (size_t i = 0; i < n; ++i) hnh[i] = next_hop[i];
+    DevTmp dtab(ctx_, table_n * sizeof(nfcs_nexthop), rc);
+    if (rc) return rc;
+    const uint32_t m = static_cast<uint32_t>(n);
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_arena_, arena, off ? off : 16))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_desc_, desc, n * sizeof(nfcs_desc)))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_ops_, hnh, n * sizeof(uint32_t)))) return rc;
+    if (table_n && (rc = nfcs_memcpy_h2d(ctx_, dtab.p, table, table_n * sizeof(nfcs_nexthop)))) return rc;
+    if ((rc = nfcs_l3_forward_device(ctx_, static_cast<uint8_t*>(d_arena_), off ? off : 16,
+                                     static_cast<nfcs_desc*>(d_desc_), static_cast<uint32_t*>(d_ops_),
+                                     m, static_cast<nfcs_nexthop*>(dtab.p), table_n,
+                                     static_cast<uint8_t*>(d_status_), nullptr)))
+        return rc;
+    if ((rc = nfcs_memcpy_d2h(ctx_, arena, d_arena_, off ? off : 16))) return rc;
+    std::vector<uint8_t> st(n);
+    if ((rc = nfcs_memcpy_d2h(ctx_, st.data(), d_status_, n))) return rc;
+    // scatter: every byte the forward writes lies below byte 128 (MACs, TTL, the IPv4 checksum,
+    // the L4 checksum at most at l2 18 + IHL 60 + 16)
+    for (size_t i = 0; i < n; ++i) {
+        if (status) status[i] = st[i];
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        if (!b || !(st[i] & NFCS_ST_FLAG_FWD)) continue;
+        const size_t len = desc[i].len, w = len < 128 ? len : 128;
+        std::memcpy(b->get_data_start_ptr(), arena + (size_t)desc[i].off16 * 16, w);
+    }
+    return NFCS_OK;
+}
+
+inline int ChecksumEngine::flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
+                                           uint32_t* hashes) {
+    if (n == 0) return NFCS_OK;
+    if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
+    std::lock_guard<std::mutex> lock(mu_);
+    // every field the key reads lies below byte 98 (l2 18 + IHL 60 + the 19-byte TcpHeader's
+    // bounds check), so the first 128 bytes with len clamped to 128 give the same key
+    int rc = reserve(n * 128 + 16, n);
+    if (rc) return rc;
+    const size_t off = gather(pkts, n, 128);
+    DevTmp dkeys(ctx_, n * sizeof(nfcs_flow_key), rc);
+    DevTmp dhash(ctx_, n * sizeof(uint32_t), rc);
+    if (rc) return rc;
+    const uint32_t m = static_cast<uint32_t>(n);
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_arena_, h_arena_, off ? off : 16))) return rc;
+    if ((rc = nfcs_memcpy_h2d(ctx_, d_desc_, h_desc_, n * sizeof(nfcs_desc)))) return rc;
+    if ((rc = nfcs_flow_keys_device(ctx_, static_cast<uint8_t*>(d_arena_), off ? off : 16,
+                                    static_cast<nfcs_desc*>(d_desc_), m,
+                                    static_cast<nfcs_flow_key*>(dkeys.p),
+                                    static_cast<uint32_t*>(dhash.p), nullptr)))
+        return rc;
+    if (keys && (rc = nfcs_memcpy_d2h(ctx_, keys, dkeys.p, n * sizeof(nfcs_flow_key)))) return rc;
+    if (hashes && (rc = nfcs_memcpy_d2h(ctx_, hashes, dhash.p, n * sizeof(uint32_t)))) return rc;
+    return NFCS_OK;
+}
+
 // Free-function form on the process-wide engine.
 inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr) {
     return ChecksumEngine::instance().update_checksums_batch(pkts, n, status);
@@ -358,6 +480,14 @@ inline int update_checksums_batch(const std::vector<Packet*>& pkts, uint8_t* sta
 inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
                       uint8_t* status = nullptr) {
     return ChecksumEngine::instance().vlan_batch(pkts, ops, n, ok, status);
+}
+inline int l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
+                            const nfcs_nexthop* table, uint32_t table_n, uint8_t* status = nullptr) {
+    return ChecksumEngine::instance().l3_forward_batch(pkts, next_hop, n, table, table_n, status);
+}
+inline int flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
+                           uint32_t* hashes = nullptr) {
+    return ChecksumEngine::instance().flow_keys_batch(pkts, n, keys, hashes);
 }
 
 }  // namespace netflow_amd

@@ -53,14 +53,17 @@ class NfcsError(RuntimeError):
     pass
 
 
-def build(verbose: bool = False, experiments: bool = False) -> str:
+def build(verbose: bool = False, experiments: bool = False, out: str | None = None,
+          extra_flags: tuple = ()) -> str:
     """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree).
     experiments=True builds netflow_amd/libnfcs_exp.so with the measurement-only ablation
-    variants (NFCS_VARIANT >= 100); the product never loads it unless NFCS_LIB points at it."""
-    out = os.path.join(HERE, "libnfcs_exp.so") if experiments else os.path.join(HERE, "libnfcs.so")
+    variants (NFCS_VARIANT >= 100); the product never loads it unless NFCS_LIB points at it.
+    out / extra_flags: measurement builds under another name with other compiler flags."""
+    if out is None:
+        out = os.path.join(HERE, "libnfcs_exp.so") if experiments else os.path.join(HERE, "libnfcs.so")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"),
-           *(["-DNFCS_EXPERIMENTS"] if experiments else []), *SOURCES, "-o", out]
+           *(["-DNFCS_EXPERIMENTS"] if experiments else []), *extra_flags, *SOURCES, "-o", out]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

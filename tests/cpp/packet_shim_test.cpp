@@ -89,10 +89,66 @@ static int vlan_mode(bool single) {
     return 0;
 }
 
+// Input: first line = the next-hop table (hex, 12 bytes per entry), then "nh hexframe" lines.
+// Output per packet: "status hex(frame)".
+static int l3_mode() {
+    std::string line;
+    if (!std::getline(std::cin, line)) return 2;
+    const std::vector<uint8_t> t = unhex(line);
+    std::vector<nfcs_nexthop> table(t.size() / sizeof(nfcs_nexthop));
+    if (!table.empty()) std::memcpy(table.data(), t.data(), table.size() * sizeof(nfcs_nexthop));
+    std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
+    std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
+    std::vector<uint32_t> nh;
+    while (std::getline(std::cin, line)) {
+        const size_t a = line.find(' ');
+        nh.push_back((uint32_t)std::stoul(line.substr(0, a)));
+        std::vector<uint8_t> f = unhex(line.substr(a + 1));
+        bufs.emplace_back(new netflow_amd::PacketBuffer(f.size() + 96, 32, f.size()));
+        if (!f.empty()) std::memcpy(bufs.back()->get_data_start_ptr(), f.data(), f.size());
+        pkts.emplace_back(new netflow_amd::Packet(bufs.back().get()));
+    }
+    std::vector<netflow_amd::Packet*> raw;
+    for (auto& p : pkts) raw.push_back(p.get());
+    std::vector<uint8_t> st(raw.size(), 0xEE);
+    int rc = netflow_amd::l3_forward_batch(raw.data(), nh.data(), raw.size(), table.data(),
+                                           (uint32_t)table.size(), st.data());
+    if (rc) { std::fprintf(stderr, "rc=%d\n", rc); return 2; }
+    for (size_t i = 0; i < raw.size(); ++i) {
+        auto* b = raw[i]->get_buffer();
+        std::printf("%d %s\n", (int)st[i], hex(b->get_data_start_ptr(), b->get_data_length()).c_str());
+    }
+    return 0;
+}
+
+// Input: one hex frame per line. Output per packet: "hash hex(64-byte record)".
+static int flow_mode() {
+    std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
+    std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::vector<uint8_t> f = unhex(line);
+        bufs.emplace_back(new netflow_amd::PacketBuffer(f.size() + 96, 32, f.size()));
+        if (!f.empty()) std::memcpy(bufs.back()->get_data_start_ptr(), f.data(), f.size());
+        pkts.emplace_back(new netflow_amd::Packet(bufs.back().get()));
+    }
+    std::vector<netflow_amd::Packet*> raw;
+    for (auto& p : pkts) raw.push_back(p.get());
+    std::vector<nfcs_flow_key> keys(raw.size());
+    std::vector<uint32_t> hashes(raw.size(), 0xEEEEEEEEu);
+    int rc = netflow_amd::flow_keys_batch(raw.data(), raw.size(), keys.data(), hashes.data());
+    if (rc) { std::fprintf(stderr, "rc=%d\n", rc); return 2; }
+    for (size_t i = 0; i < raw.size(); ++i)
+        std::printf("%u %s\n", hashes[i], hex(reinterpret_cast<const uint8_t*>(&keys[i]), sizeof(nfcs_flow_key)).c_str());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (mode == "cpu") return cpu_checks();
     if (mode == "vlan" || mode == "vlan1") return vlan_mode(mode == "vlan1");
+    if (mode == "l3") return l3_mode();
+    if (mode == "flow") return flow_mode();
     std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
     std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
     std::string line;

@@ -86,3 +86,46 @@ def test_cpp_vlan_matches_reference_behaviour(exe, mode):
         assert hx == buf[:room[i]].tobytes().hex(), i
         if mode == "vlan":
             assert int(st) == est, i
+
+
+@pytest.mark.gpu
+def test_cpp_l3_forward_matches_oracle(exe):
+    """netflow_amd::l3_forward_batch against the oracle (pinned to the reference's switch data
+    path by tests/golden/kat_l3.json / l3fwd_ref.npz): frame bytes and status per packet."""
+    import numpy as np
+    frames = _frames()
+    rng = np.random.default_rng(9)
+    table = rng.integers(0, 256, size=(4, 12), dtype=np.uint8)
+    nh = [int(x) for x in (np.arange(len(frames)) % 5)]  # 4 = no route
+    inp = table.tobytes().hex() + "\n" + "\n".join(f"{h} {f.hex()}" for h, f in zip(nh, frames)) + "\n"
+    r = subprocess.run([exe, "l3"], input=inp, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(frames)
+    arena, desc = oracle.pack_frames(frames)
+    rst = oracle.l3_forward_batch(arena, desc, np.array(nh, dtype=np.uint32), table)
+    for i, (f, line) in enumerate(zip(frames, lines)):
+        st, hx = (line.split(" ") + [""])[:2]
+        if (rst[i] & 0x3F) == 14:
+            continue
+        o = int(desc[i]["off16"]) * 16
+        assert hx == arena[o:o + len(f)].tobytes().hex(), i
+        assert int(st) == int(rst[i]), i
+
+
+@pytest.mark.gpu
+def test_cpp_flow_keys_match_oracle(exe):
+    """netflow_amd::flow_keys_batch against the oracle (pinned to the reference's
+    packet_classifier.cpp by tests/golden/kat_flow.json / flow_ref.npz), frames of all lengths
+    (only the first 128 bytes travel)."""
+    frames = _frames() + oracle.fuzz_frames(5150, 0, 500)
+    r = subprocess.run([exe, "flow"], input="\n".join(f.hex() for f in frames) + "\n",
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(frames)
+    for i, (f, line) in enumerate(zip(frames, lines)):
+        h, rec = line.split(" ")
+        erec, eh = oracle.flow_key(f)
+        assert int(h) == eh, i
+        assert rec == erec.hex(), i
