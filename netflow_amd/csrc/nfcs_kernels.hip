@@ -782,7 +782,12 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                 uint2 r;
                 r.x = (ipw_ & 0xFFFFu) | (l4w_ << 16);
                 r.y = (ipw_ >> 16) | (l4w_ & 0xFFFF0000u);
-                ((uint2*)patch)[S.p] = r;
+                uint2* q = (uint2*)patch + S.p;
+                if (DBG & 65536) __builtin_nontemporal_store(((uint64_t)r.y << 32) | r.x, (uint64_t*)q);
+                else if (DBG & 131072)
+                    __hip_atomic_store((uint64_t*)q, ((uint64_t)r.y << 32) | r.x, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else *q = r;
             }
         }
     };
@@ -1133,6 +1138,22 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 83: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 7, false, 1, 64>),
                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                 base16, status, patch, nofwd); break;  // 29 with plain stores
+    case 10:
+    case 11: {  // split mode, pass 1 writing its patch records non-temporal / write-through
+        nfcs_patch* pp = patch ? patch : ws;
+        if (!pp) return hipErrorInvalidValue;
+        if (variant == 10)
+            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1 | 65536, 1, false, 1>), dim3(rows_grid(16)),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
+        else
+            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1 | 131072, 1, false, 1>), dim3(rows_grid(16)),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
+        int ga = (int)((n + kBlock - 1) / kBlock);
+        if (ga > di.cus * 8) ga = di.cus * 8;
+        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
+                           base16, pp);
+        break;
+    }
     case 9: {  // split mode with a write-through patch pass
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
