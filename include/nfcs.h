@@ -43,7 +43,9 @@ extern "C" {
  * Replaces PacketBuffer's data window [get_data_start_ptr(), +get_data_length())
  * (packet_buffer.hpp:51-52). Frames start on 16-byte boundaries; the arena must cover
  * off16*16 + round_up(len, 16) bytes for every descriptor (the kernel reads whole 16-byte
- * chunks; a descriptor outside the arena is rejected per packet with NFCS_ST_BAD_DESC). */
+ * chunks; a descriptor outside the arena is rejected per packet with NFCS_ST_BAD_DESC).
+ * Frames of one batch must not overlap (as separate PacketBuffers never do): the kernels may
+ * rewrite a frame's own 16-byte chunks whole, with the values they read from them. */
 typedef struct nfcs_desc {
     uint32_t off16; /* frame start, in 16-byte units from the arena base */
     uint32_t len;   /* frame length in bytes (PacketBuffer::data_len_)     */
