@@ -25,6 +25,7 @@
 // Header-only; link with -lnfcs (netflow_amd/libnfcs.so).
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
@@ -58,7 +59,22 @@ struct PacketBuffer {
             throw std::invalid_argument("Initial headroom + data length exceeds capacity");
         }
     }
-    ~PacketBuffer() { delete[] raw_data_ptr_; }
+    // Non-owning form: the bytes belong to someone else (a BufferPool's pinned arena slot).
+    struct External {};
+    PacketBuffer(External, unsigned char* storage, size_t capacity, size_t initial_headroom = 0,
+                 size_t initial_data_len = 0)
+        : raw_data_ptr_(storage),
+          capacity_(capacity),
+          data_offset_(initial_headroom),
+          data_len_(initial_data_len),
+          ref_count(1),
+          owns_(false) {
+        if (initial_headroom + initial_data_len > capacity)
+            throw std::invalid_argument("Initial headroom + data length exceeds capacity");
+    }
+    ~PacketBuffer() {
+        if (owns_) delete[] raw_data_ptr_;
+    }
     PacketBuffer(const PacketBuffer&) = delete;
     PacketBuffer& operator=(const PacketBuffer&) = delete;
 
@@ -102,6 +118,8 @@ struct PacketBuffer {
             throw std::out_of_range("New offset and length exceed buffer capacity in reset_offsets_and_len");
         }
     }
+
+    bool owns_ = true;  // false: storage not allocated by this buffer
 };
 
 class Packet;
@@ -159,6 +177,13 @@ public:
                                uint32_t* hashes = nullptr);
 
     nfcs_ctx* ctx() const { return ctx_; }
+
+    // nfcs_update_host on this engine's context, serialised with its other calls.
+    int update_host(uint8_t* h_arena, uint64_t arena_bytes, const nfcs_desc* h_desc, uint32_t n,
+                    uint8_t* h_status, uint32_t flags) {
+        std::lock_guard<std::mutex> lock(mu_);
+        return nfcs_update_host(ctx_, h_arena, arena_bytes, h_desc, n, h_status, flags);
+    }
 
 private:
     // A device buffer for one call (next-hop tables, flow-key records).
@@ -467,6 +492,128 @@ inline int ChecksumEngine::flow_keys_batch(Packet* const* pkts, size_t n, nfcs_f
         return rc;
     if (keys && (rc = nfcs_memcpy_d2h(ctx_, keys, dkeys.p, n * sizeof(nfcs_flow_key)))) return rc;
     if (hashes && (rc = nfcs_memcpy_d2h(ctx_, hashes, dhash.p, n * sizeof(uint32_t)))) return rc;
+    return NFCS_OK;
+}
+
+// Same interface as netflow::BufferPool (buffer_pool.hpp:57-123: allocate_buffer(payload,
+// headroom), free_buffer(buffer) with the PacketBuffer reference count), except that every
+// buffer up to slot_bytes is a slot of ONE pinned arena (nfcs_host_alloc). A burst whose buffers
+// come from the pool is checksummed with no gather copy: update_checksums_batch builds the
+// descriptors straight into the arena and calls nfcs_update_host on it (frames DMA'd from the
+// pinned arena, patch records back; or, with NFCS_HOST_ZERO_COPY, read by the kernel over PCIe
+// in place). Buffers larger than a slot are heap PacketBuffers, as the reference allocates them.
+class BufferPool {
+public:
+    explicit BufferPool(size_t slots = 65536, size_t slot_bytes = 2048,
+                        ChecksumEngine& engine = ChecksumEngine::instance())
+        : eng_(engine), slots_(slots), slot_bytes_((slot_bytes + 15) & ~size_t(15)) {
+        if (slots_ == 0 || slots_ * slot_bytes_ / 16 > 0xFFFFFFFFull)
+            throw std::invalid_argument("BufferPool: slots x slot_bytes must address < 64 GiB");
+        void* p = nullptr;
+        const int rc = nfcs_host_alloc(eng_.ctx(), slots_ * slot_bytes_, &p);
+        if (rc != NFCS_OK) throw std::bad_alloc();
+        arena_ = static_cast<unsigned char*>(p);
+        bufs_.reserve(slots_);
+        free_.reserve(slots_);
+        for (size_t i = 0; i < slots_; ++i) {
+            bufs_.emplace_back(new PacketBuffer(PacketBuffer::External{}, arena_ + i * slot_bytes_, slot_bytes_));
+            free_.push_back(static_cast<uint32_t>(slots_ - 1 - i));  // allocate in arena order
+        }
+    }
+    ~BufferPool() {
+        std::lock_guard<std::mutex> lock(mu_);
+        for (PacketBuffer* b : heap_free_) delete b;
+        bufs_.clear();
+        nfcs_host_free(eng_.ctx(), arena_);
+    }
+    BufferPool(const BufferPool&) = delete;
+    BufferPool& operator=(const BufferPool&) = delete;
+
+    // buffer_pool.hpp:66-103: data length 0, the given headroom, reference count 1.
+    PacketBuffer* allocate_buffer(size_t required_data_payload_size, size_t required_headroom = 32) {
+        std::lock_guard<std::mutex> lock(mu_);
+        const size_t need = required_data_payload_size + required_headroom;
+        if (need <= slot_bytes_ && !free_.empty()) {
+            PacketBuffer* b = bufs_[free_.back()].get();
+            free_.pop_back();
+            b->ref_count.store(1, std::memory_order_relaxed);
+            b->reset_offsets_and_len(required_headroom, 0);
+            return b;
+        }
+        for (auto it = heap_free_.begin(); it != heap_free_.end(); ++it) {
+            if ((*it)->get_capacity() >= need) {
+                PacketBuffer* b = *it;
+                heap_free_.erase(it);
+                b->ref_count.store(1, std::memory_order_relaxed);
+                b->reset_offsets_and_len(required_headroom, 0);
+                return b;
+            }
+        }
+        return new PacketBuffer(need, required_headroom, 0);
+    }
+
+    // buffer_pool.hpp:106-123: back to the pool when the last reference is released.
+    void free_buffer(PacketBuffer* buffer) {
+        if (!buffer || !buffer->decrement_ref()) return;
+        std::lock_guard<std::mutex> lock(mu_);
+        if (in_arena(buffer)) free_.push_back(slot_of(buffer));
+        else heap_free_.push_back(buffer);
+    }
+
+    bool in_arena(const PacketBuffer* b) const {
+        return b && b->raw_data_ptr_ >= arena_ && b->raw_data_ptr_ < arena_ + slots_ * slot_bytes_;
+    }
+    size_t available() {
+        std::lock_guard<std::mutex> lock(mu_);
+        return free_.size();
+    }
+    unsigned char* arena() const { return arena_; }
+
+    // Batched Packet::update_checksums() on packets whose buffers are pool slots with 16-byte
+    // aligned data starts (the default headroom of 32 keeps them aligned): no gather or scatter
+    // copies. Other packets make the call fall back to ChecksumEngine::update_checksums_batch.
+    // flags: 0 (frames DMA'd from the pinned arena) or NFCS_HOST_ZERO_COPY.
+    int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr,
+                               uint32_t flags = 0);
+
+private:
+    uint32_t slot_of(const PacketBuffer* b) const {
+        return static_cast<uint32_t>((b->raw_data_ptr_ - arena_) / slot_bytes_);
+    }
+
+    ChecksumEngine& eng_;
+    size_t slots_, slot_bytes_;
+    unsigned char* arena_ = nullptr;
+    std::vector<std::unique_ptr<PacketBuffer>> bufs_;
+    std::vector<uint32_t> free_;
+    std::vector<PacketBuffer*> heap_free_;
+    std::mutex mu_;
+};
+
+inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status,
+                                              uint32_t flags) {
+    if (n == 0) return NFCS_OK;
+    if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
+    std::vector<std::pair<uint32_t, uint32_t>> order(n);  // (off16, packet index)
+    std::vector<nfcs_desc> desc(n);
+    for (size_t i = 0; i < n; ++i) {
+        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        const unsigned char* d = b ? b->get_data_start_ptr() : nullptr;
+        if (!b || !in_arena(b) || ((d - arena_) & 15))
+            return eng_.update_checksums_batch(pkts, n, status);
+        order[i] = {static_cast<uint32_t>((d - arena_) >> 4), static_cast<uint32_t>(i)};
+    }
+    std::sort(order.begin(), order.end());  // nfcs_update_host takes frames in arena order
+    for (size_t j = 0; j < n; ++j) {
+        PacketBuffer* b = pkts[order[j].second]->get_buffer();
+        desc[j] = nfcs_desc{order[j].first, static_cast<uint32_t>(b->get_data_length())};
+    }
+    std::vector<uint8_t> st(status ? n : 0);
+    const int rc = eng_.update_host(arena_, slots_ * slot_bytes_, desc.data(), static_cast<uint32_t>(n),
+                                    status ? st.data() : nullptr, flags);
+    if (rc) return rc;
+    if (status)
+        for (size_t j = 0; j < n; ++j) status[order[j].second] = st[j];
     return NFCS_OK;
 }
 

@@ -129,3 +129,26 @@ def test_cpp_flow_keys_match_oracle(exe):
         erec, eh = oracle.flow_key(f)
         assert int(h) == eh, i
         assert rec == erec.hex(), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pool", "poolzc"])
+def test_cpp_buffer_pool_batch_matches_oracle(exe, mode):
+    """netflow_amd::BufferPool (buffer_pool.hpp:57-123 semantics, slots of one pinned arena):
+    a burst checksummed in place with no gather copy (poolzc: the kernel reads the pinned
+    arena over PCIe), bit-exact with the oracle; allocate / free / refcount behaviour."""
+    frames = _frames()[:3000]
+    r = subprocess.run([exe, mode], input="\n".join(f.hex() for f in frames) + "\n",
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "pool_failures=0" in r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(frames)
+    for f, line in zip(frames, lines):
+        st, hx = (line.split(" ") + [""])[:2]
+        exp, est = oracle.update_frame(f)
+        if (est & 0x3F) == 14:
+            assert hx == f.hex()
+            continue
+        assert hx == exp.hex()
+        assert int(st) == est
