@@ -601,10 +601,19 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     if (FWD) __builtin_amdgcn_sched_barrier(0);
 }
 
-// DBG (measurement builds only, NFCS_EXPERIMENTS): 1 = no frame stores, 2 = fixed C1 plan
-// (no parse), 3 = both; 4 = s_setprio 3 over the compute phase; 8 = s_setprio 3 over load issue.
-// Measurement builds (DBG 256): per-wave timeline. s_memtime returns the shader clock; the
-// trailing lgkmcnt(0) makes the stamp wait for every scalar load issued before it.
+// DBG bits of update_rows_kernel. The product instantiates DBG 0 (and 1 for split mode's first
+// pass); every other value exists only in measurement builds (NFCS_EXPERIMENTS, variants in
+// launch_update / launch_l3_forward; results in profiles/r01_s2_variants.md):
+//        1  no frame stores (split mode's first pass writes patch records only)
+//        2  fixed C1 plan, no parse                  4 / 8  s_setprio 3 over compute / load issue
+//       16  L3 forward: no next-hop index loads      64 / 128  descriptor prefetch 16k / 64k ahead
+//      256  per-wave timeline stamps into `patch`    512 / 1024 / 4096  nt / sc0 sc1 / sc0 sc1 nt
+//     8192  plain (write-back) frame stores               checksum stores
+//    16384  one write-through segment store per packet (the L3 forward's default form)
+//    32768  L3 forward: 16-byte + byte stores instead of the segment store
+//    65536 / 131072  patch records stored nt / write-through
+// Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
+// wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
     uint64_t t;
     __builtin_amdgcn_sched_barrier(0);
