@@ -1726,8 +1726,8 @@ DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uin
     if (hashes && rl == 0 && p < n) hashes[p] = hv;
 }
 
-template <int K, int ST = 1, int LD = 0>
-__global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __restrict__ arena,
+template <int K, int ST = 1, int LD = 0, int BS = kBlock>
+__global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            const nfcs_desc* __restrict__ desc,
                                                            uint32_t n, nfcs_flow_key* __restrict__ keys,
@@ -1737,7 +1737,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_kernel(const uint8_t* __rest
     constexpr uint32_t PR = 64 / R, PW = PR * K;  // rows per wave, packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = ((uint64_t)blockIdx.x * (kBlock / 64) + rfl(threadIdx.x >> 6)) * PW;
+    const uint64_t pw = ((uint64_t)blockIdx.x * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
     if (pw >= n) return;
     uint2 dl = make_uint2(0u, 0u);  // lane l: descriptor of packet pw + l
     if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
@@ -1775,6 +1775,19 @@ hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t ar
     case 84: NFCS_FK(4, 0, 0); break;  // plain record stores (nt: C1 +1.5-2%)
     case 85: NFCS_FK(4, 2, 0); break;  // write-through record stores
     case 86: NFCS_FK(4, 1, 1); break;  // ... and non-temporal header loads
+#define NFCS_FKB(K, BS)                                                                           \
+    hipLaunchKernelGGL((flow_keys_kernel<K, 1, 0, BS>), dim3((n + (BS / 8) * K - 1u) / ((BS / 8) * K)), \
+                       dim3(BS), 0, stream, arena, arena_bytes, desc, n, keys, hashes)
+    case 90: NFCS_FKB(4, 64); break;   // one-wave workgroups
+    case 91: NFCS_FKB(4, 128); break;
+    case 92: NFCS_FKB(4, 512); break;
+    case 93: NFCS_FKB(2, 64); break;
+    case 94: NFCS_FKB(8, 64); break;
+    case 95: NFCS_FKB(1, 64); break;
+    case 96: NFCS_FKB(2, 128); break;
+    case 97: NFCS_FKB(3, 64); break;
+    case 98: NFCS_FKB(2, 256); break;
+#undef NFCS_FKB
 #endif
     default: NFCS_FK(4, 1, 0); break;  // 32 packets per wave, non-temporal record stores
     }
