@@ -1195,6 +1195,15 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 87: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // 80 at 7 waves/SIMD
+    case 121: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // short-frame form, no parse
+    case 122: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 3, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // ... and no frame stores
+    case 123: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // short-frame form, no stores
     case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // every slot non-temporal (header too)
