@@ -822,7 +822,8 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                     if ((pos >> 4) == rl) v = put_byte(v, pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
                 }
             }
-            if (any && rl <= last) st16<true>((uint4*)frame + rl, v);
+            if (DBG & 262144) last = max(last, 3u);  // measurement: a whole 64-byte half line
+            if (any && rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
         }
         emit(S.valid && !slow, st, ipw, l4w, false);
     } else {
@@ -1204,6 +1205,12 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 123: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1, 64>),
                                  dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                  base16, status, patch, nofwd); break;  // short-frame form, no stores
+    case 89: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384 | 262144, 1, false, 1, 256>),
+                                dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
+                                base16, status, patch, nofwd); break;  // segment store = full 64 B
+    case 125: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384 | 262144, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // ... short-frame form
     case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // every slot non-temporal (header too)
