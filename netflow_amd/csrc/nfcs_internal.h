@@ -50,8 +50,8 @@ constexpr uint64_t kSplitMeanBytes = 2048;
 // granularity loss (C3 +2-3%, profiles/r01_s2_variants.md run bs1/bs2).
 constexpr uint64_t kSmallMeanBytes = 1200;
 inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
-    return variant == 8 || variant == 9 || variant == 10 || variant == 11 || variant == 12 ||
-           variant == 22 || variant == 23 ||  // 9-12, 22, 23: experiments build only
+    return variant == 8 || (variant >= 9 && variant <= 14) || variant == 22 ||
+           variant == 23 ||  // 9-14, 22, 23: experiments build only
            (variant == 0 && n > 0 && arena_bytes / n >= kSplitMeanBytes);
 }
 // variants that stage patch records in a context workspace (split mode)

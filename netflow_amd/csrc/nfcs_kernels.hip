@@ -1148,11 +1148,20 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 83: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 7, false, 1, 64>),
                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                 base16, status, patch, nofwd); break;  // 29 with plain stores
-    case 12: {  // split mode, pass 1 held at 7 waves/SIMD (94 SGPRs)
+    case 13:
+    case 14:
+    case 12: {  // split mode, pass 1 held at 7 waves/SIMD (94 SGPRs) / with 8 / 12 slots per batch
         nfcs_patch* pp = patch ? patch : ws;
         if (!pp) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1>), dim3(rows_grid(16)),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
+        if (variant == 13)
+            hipLaunchKernelGGL((update_rows_kernel<8, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
+        else if (variant == 14)
+            hipLaunchKernelGGL((update_rows_kernel<12, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
+        else
+            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1>), dim3(rows_grid(16)),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
         int ga = (int)((n + kBlock - 1) / kBlock);
         if (ga > di.cus * 8) ga = di.cus * 8;
         hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
