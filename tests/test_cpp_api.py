@@ -152,3 +152,21 @@ def test_cpp_buffer_pool_batch_matches_oracle(exe, mode):
             continue
         assert hx == exp.hex()
         assert int(st) == est
+
+
+def test_cpp_api_host_code_under_asan_ubsan():
+    """the C++ host API (PacketBuffer / Packet semantics, the engine's refusal to
+    run without a device) compiled with -fsanitize=address,undefined (host code only)."""
+    if not os.path.exists(nf.LIB_PATH):
+        nf.build()
+    libdir = os.path.dirname(nf.LIB_PATH)
+    exe = os.path.join(ROOT, "tests", "cpp", "packet_shim_test_asan")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+                    "-I" + os.path.join(ROOT, "include"), SRC, "-o", exe, "-L" + libdir,
+                    "-l:" + os.path.basename(nf.LIB_PATH), "-Wl,-rpath," + libdir,
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")  # the HIP runtime's own allocations
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode in (0,) and "api_failures=0" in r.stdout, r.stdout + r.stderr[-3000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr

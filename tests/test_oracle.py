@@ -131,3 +131,19 @@ def test_c4_shard_digest_matches_reference(oracle_lib):
     assert (sh["first"], sh["n"]) == (7 << 22, 1 << 22)
     din, dout, _ = oracle.config_digest(1, 20250620, sh["first"], sh["n"], 8)
     assert (f"{din:016x}", f"{dout:016x}") == (sh["digest_in"], sh["digest_out"])
+
+
+def test_oracle_under_asan_ubsan():
+    """the CPU restatement built with -fsanitize=address,undefined runs every
+    entry point over 200k fuzz frames held in exact-size heap buffers without a finding."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "sanitize"], check=True)
+    r = subprocess.run([os.path.join(here, "_san", "nfo_sanitize"), "200000", "9090"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "sanitize_frames=200000" in r.stdout
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
