@@ -37,6 +37,14 @@ namespace nfcs {
 #define DEV __device__ __forceinline__
 
 DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin; this bijection on
+// [0, gridDim.x) gives each XCD one contiguous eighth of the blocks (the tail beyond a
+// multiple of 8 keeps its order).
+DEV uint32_t xcd_block() {
+    const uint32_t b = blockIdx.x, g8 = gridDim.x / 8u;
+    return b < 8u * g8 ? (b % 8u) * g8 + b / 8u : b;
+}
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
 __device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
@@ -612,6 +620,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //    16384  one write-through segment store per packet (the L3 forward's default form)
 //    32768  L3 forward: 16-byte + byte stores instead of the segment store
 //    65536 / 131072  patch records stored nt / write-through
+//  2097152 / 4194304  XCD order in chunks of 64 / 8 blocks   8388608  dispatch order (no remap)
 // Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
 // wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
@@ -926,7 +935,24 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
     const uint32_t stride = gridDim.x * (BS / R);
-    const uint64_t w0 = (uint64_t)blockIdx.x * (BS / R) + rfl(threadIdx.x >> 6) * PW;
+    // XCD-aware block order (session 3): workgroups are dealt to the 8 XCDs round-robin;
+    // remapped, the workgroups one XCD runs take one contiguous eighth of the batch, so each
+    // XCD streams its own region of HBM and the descriptor lines its workgroups share stay in
+    // its L2 (a bijection on [0, gridDim.x); the tail beyond a multiple of 8 keeps its order).
+    // C1 +1.3%, C3 +0.5%, measured (variants 129/128 at the time; DBG 8388608 turns it off).
+    uint32_t bid = blockIdx.x;
+    if (!(DBG & (8388608 | 2097152 | 4194304))) {
+        const uint32_t g8 = gridDim.x / 8u;
+        if (bid < 8u * g8) bid = (bid % 8u) * g8 + bid / 8u;
+    } else if (DBG & (2097152 | 4194304)) {  // measurement: chunks of C blocks dealt round-robin
+        constexpr uint32_t C = (DBG & 2097152) ? 64u : 8u;
+        const uint32_t full = gridDim.x / (8u * C) * (8u * C);
+        if (bid < full) {
+            const uint32_t x = bid % 8u, k = bid / 8u;
+            bid = ((k / C) * 8u + x) * C + k % C;
+        }
+    }
+    const uint64_t w0 = (uint64_t)bid * (BS / R) + rfl(threadIdx.x >> 6) * PW;
     if (w0 >= n) return;
     // Fused L3 forward: the wave's PW next-hop indexes and their table rows are wave-uniform.
     // Read through the constant address space they are scalar loads on lgkmcnt, issued with the
@@ -1220,6 +1246,21 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 125: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384 | 262144, 7, false, 1, 64>),
                                  dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                  base16, status, patch, nofwd); break;  // ... short-frame form
+    case 128: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8388608, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // short-frame form, dispatch order
+    case 129: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8388608, 1, false, 1, 256>),
+                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // C1 form, dispatch order
+    case 130: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2097152, 1, false, 1, 256>),
+                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // C1 form, 64-block chunks
+    case 132: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 4194304, 1, false, 1, 256>),
+                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // C1 form, 8-block chunks
+    case 133: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2097152, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // C3 form, 64-block chunks
     case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // every slot non-temporal (header too)
@@ -1436,7 +1477,7 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K, int K2 = 2, bool WT = false, bool NTS = false>
+template <int K, int K2 = 2, bool WT = false, bool NTS = false, bool XR = false>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1449,7 +1490,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     constexpr uint32_t PW = 4, KR = (uint32_t)(K * R);
     const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
     const uint32_t rowbase4 = (lane & ~15u) * 4u;
-    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    const uint64_t pw = (uint64_t)(XR ? xcd_block() : blockIdx.x) * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
     const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
     uint32_t op = op_all, cap = cap_all;
@@ -1645,6 +1686,9 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((vlan_rows_kernel<6, 2, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
                            arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
 #ifdef NFCS_EXPERIMENTS
+    else if (variant == 34)  // XCD-aware block order (measured 2% slower here: not adopted)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, false, true>), dim3(blocks), dim3(kBlock), di.lds_pad,
+                           stream, arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     else if (variant == 33)  // non-temporal chunk stores (checksum bytes written through)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, true>), dim3(blocks), dim3(kBlock), di.lds_pad,
                            stream, arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
@@ -1751,7 +1795,7 @@ DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uin
     if (hashes && rl == 0 && p < n) hashes[p] = hv;
 }
 
-template <int K, int ST = 1, int LD = 0, int BS = kBlock>
+template <int K, int ST = 1, int LD = 0, int BS = kBlock, bool XR = false>
 __global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            const nfcs_desc* __restrict__ desc,
@@ -1762,7 +1806,7 @@ __global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict
     constexpr uint32_t PR = 64 / R, PW = PR * K;  // rows per wave, packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = ((uint64_t)blockIdx.x * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
+    const uint64_t pw = ((uint64_t)(XR ? xcd_block() : blockIdx.x) * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
     if (pw >= n) return;
     uint2 dl = make_uint2(0u, 0u);  // lane l: descriptor of packet pw + l
     if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
@@ -1812,9 +1856,15 @@ hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t ar
     case 96: NFCS_FKB(2, 128); break;
     case 97: NFCS_FKB(3, 64); break;
     case 98: NFCS_FKB(2, 256); break;
+    case 99: hipLaunchKernelGGL((flow_keys_kernel<4, 1, 0, kBlock, false>), dim3((n + 127u) / 128u),
+                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
+        break;  // dispatch order (no XCD remap)
 #undef NFCS_FKB
 #endif
-    default: NFCS_FK(4, 1, 0); break;  // 32 packets per wave, non-temporal record stores
+    default:  // 32 packets per wave, non-temporal record stores, XCD-aware block order (+1.5-2%)
+        hipLaunchKernelGGL((flow_keys_kernel<4, 1, 0, kBlock, true>), dim3((n + 127u) / 128u),
+                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
+        break;
     }
 #undef NFCS_FK
     return hipGetLastError();
