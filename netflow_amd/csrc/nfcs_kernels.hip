@@ -577,7 +577,7 @@ struct FwdArgs {
     uint32_t table_n;
 };
 
-template <int K, int NT, int R = 16, bool FWD = false>
+template <int K, int NT, int R = 16, bool FWD = false, bool SKIP = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
                    uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0,
                    const FwdArgs* fa = nullptr) {
@@ -595,13 +595,16 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
     // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
+    // (SKIP, measurement: slots past every row's frame in the wave are not issued at all)
+    const uint32_t wmax = SKIP ? wave_max_rows<R>(nch) : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k;
         const uint4* a = (c < nch) ? src + c : &g_zero16;
         // NT 2: the header slot keeps the default policy so its lines are still in L2 when
         // the checksum chunks are written back; payload slots stream through as evict-first
-        S.v[k] = (NT == 2 && k == 0) ? ld16<0>(a) : ld16<NT>(a);
+        if (SKIP && k > 0 && (uint32_t)R * k >= wmax) S.v[k] = make_uint4(0u, 0u, 0u, 0u);
+        else S.v[k] = (NT == 2 && k == 0) ? ld16<0>(a) : ld16<NT>(a);
     }
     // all K loads issue before any use of the header slot: without this fence the scheduler
     // hoists the forward decision's first DPP read above the last loads of the FWD kernel and
@@ -621,6 +624,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //    32768  L3 forward: 16-byte + byte stores instead of the segment store
 //    65536 / 131072  patch records stored nt / write-through
 //  2097152 / 4194304  XCD order in chunks of 64 / 8 blocks   8388608  dispatch order (no remap)
+// 16777216  slots past every row's frame not issued (wave-uniform branches)
 // Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
 // wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
@@ -1022,7 +1026,7 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
             }
         }
         if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
-        row_stage<K, NT, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
+        row_stage<K, NT, R, FWD, (DBG & 16777216) != 0>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
                                  rl, nh, &fa);
         if (DBG & 8) __builtin_amdgcn_s_setprio(0);
         row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac, T);
@@ -1261,6 +1265,12 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     case 133: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2097152, 7, false, 1, 64>),
                                  dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
                                  base16, status, patch, nofwd); break;  // C3 form, 64-block chunks
+    case 134: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16777216, 7, false, 1, 64>),
+                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // short-frame form, skip empty slots
+    case 135: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16777216, 1, false, 1, 256>),
+                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
+                                 base16, status, patch, nofwd); break;  // C1 form, skip empty slots
     case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
                                 dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
                                 patch, nofwd); break;  // every slot non-temporal (header too)
