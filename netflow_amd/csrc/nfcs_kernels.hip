@@ -1130,252 +1130,8 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
                            base16, pp);
         break;
     }
-#ifdef NFCS_EXPERIMENTS  // ablations for measurement builds (libnfcs_exp.so) only
-    case 27: NFCS_ROWS(6, 2, 16); break;  // as 0 with per-slot masked boundary chunks (round-1 v3d)
-    case 1: NFCS_ROWS(6, 0, 16); break;   // all loads default policy
-    case 2: NFCS_ROWS(4, 2, 16); break;   // 4 slots (1 KiB per batch)
-    case 4: NFCS_ROWS(6, 1, 16); break;   // all loads evict-first
-    case 5: NFCS_ROWS(12, 2, 8); break;   // 8-lane rows, 12 slots: 8 packets per wave
-    case 25: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8-lane rows K=6, branch-free sums
-    case 26: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 1, false, 1>), dim3(rows_grid(8)),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8-lane rows K=12, branch-free sums
-#define NFCS_ROWS_BS(BS)                                                                          \
-    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1, BS>),                         \
-                       dim3((n + (BS / 16) - 1) / (BS / 16)), dim3(BS), 0, stream, arena, arena_bytes, \
-                       desc, n, base16, status, patch, nofwd)
-    // occupancy-bounded forms: update_rows_kernel<K, NT, R, DBG, OCC, FWD, SV, BS>
-    case 70: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 8, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8 waves per SIMD (64 VGPRs)
-    case 71: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 8, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // ... one-wave workgroups
-    case 72: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 7, false, 1, 256>), dim3(rows_grid(8)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 8-lane rows K=6 at 7 waves per SIMD
-    case 73: hipLaunchKernelGGL((update_rows_kernel<6, 2, 8, 0, 7, false, 1, 64>),
-                                dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // ... one-wave workgroups
-    case 75: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // default held at 7 waves/SIMD (SGPRs <= 96)
-    case 76: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 64>),
-                                dim3(grid > 0 && (uint32_t)grid < (n + 3u) / 4u ? (uint32_t)grid : (n + 3u) / 4u),
-                                dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
-                                nofwd); break;  // 29 with a grid-stride loop when NFCS_GRID is set
-    case 79: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 512, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // default with non-temporal checksum stores
-    case 80: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // ... system-scope (write-through) stores
-    case 84: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // plain (write-back) checksum stores, sessions 1-2
-    case 83: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 29 with plain stores
-    case 13:
-    case 14:
-    case 12: {  // split mode, pass 1 held at 7 waves/SIMD (94 SGPRs) / with 8 / 12 slots per batch
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        if (variant == 13)
-            hipLaunchKernelGGL((update_rows_kernel<8, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
-        else if (variant == 14)
-            hipLaunchKernelGGL((update_rows_kernel<12, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
-        else
-            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1>), dim3(rows_grid(16)),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
-    }
-    case 10:
-    case 11: {  // split mode, pass 1 writing its patch records non-temporal / write-through
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        if (variant == 10)
-            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1 | 65536, 1, false, 1>), dim3(rows_grid(16)),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
-        else
-            hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1 | 131072, 1, false, 1>), dim3(rows_grid(16)),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp, nofwd);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
-    }
-    case 9: {  // split mode with a write-through patch pass
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
-                           nofwd);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel<true>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
-    }
-    case 85: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 4096, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // ... sc0 sc1 nt
-    case 86: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 29 with system-scope stores
-    case 87: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1024, 7, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // 80 at 7 waves/SIMD
-    case 121: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // short-frame form, no parse
-    case 122: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 3, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // ... and no frame stores
-    case 123: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // short-frame form, no stores
-    case 89: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384 | 262144, 1, false, 1, 256>),
-                                dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // segment store = full 64 B
-    case 125: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384 | 262144, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // ... short-frame form
-    case 128: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8388608, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // short-frame form, dispatch order
-    case 129: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8388608, 1, false, 1, 256>),
-                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // C1 form, dispatch order
-    case 130: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2097152, 1, false, 1, 256>),
-                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // C1 form, 64-block chunks
-    case 132: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 4194304, 1, false, 1, 256>),
-                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // C1 form, 8-block chunks
-    case 133: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 2097152, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // C3 form, 64-block chunks
-    case 134: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16777216, 7, false, 1, 64>),
-                                 dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // short-frame form, skip empty slots
-    case 135: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16777216, 1, false, 1, 256>),
-                                 dim3(rows_grid(16)), dim3(256), 0, stream, arena, arena_bytes, desc, n,
-                                 base16, status, patch, nofwd); break;  // C1 form, skip empty slots
-    case 96: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // every slot non-temporal (header too)
-    case 97: hipLaunchKernelGGL((update_rows_kernel<6, 1, 16, 0, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // ... short-frame form
-    case 98: hipLaunchKernelGGL((update_rows_kernel<6, 0, 16, 0, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // every slot default policy
-    case 94: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // one write-through segment store per packet
-    case 95: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 16384, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // ... in the short-frame form
-    case 77: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 76 + descriptor prefetch 16k ahead
-    case 78: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // ... 64k ahead
-    case 74: hipLaunchKernelGGL((update_rows_kernel<12, 2, 8, 0, 5, false, 1, 64>),
-                                dim3((n + 7u) / 8u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 8-lane K=12, 5 waves per SIMD
-    case 64: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // descriptor prefetch 16k packets ahead
-    case 65: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 1, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // ... 64k packets ahead
-    case 66: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 64, 1, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 16k ahead, one-wave groups
-    case 67: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 128, 1, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;  // 64k ahead, one-wave groups
-    // per-wave timeline (tools/wave_timeline.py): `patch` = 8 u64 per wave
-    case 90: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 256, 7, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;
-    case 91: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 256, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;
-    case 92: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 257, 7, false, 1, 256>), dim3(rows_grid(16)),
-                                dim3(256), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;  // ... no frame stores
-    case 93: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 257, 7, false, 1, 64>),
-                                dim3((n + 3u) / 4u), dim3(64), 0, stream, arena, arena_bytes, desc, n,
-                                base16, status, patch, nofwd); break;
-    case 60: NFCS_ROWS_BS(64); break;    // default kernel, one wave per workgroup
-    case 61: NFCS_ROWS_BS(128); break;
-    case 62: NFCS_ROWS_BS(512); break;
-    case 63: NFCS_ROWS_BS(1024); break;
-#undef NFCS_ROWS_BS
-    case 50: case 51: case 52: case 53: {  // pipelined row kernel, grid = waves per SIMD x SIMDs
-        const int wps = variant - 48;        // 2..5 waves per SIMD
-        const uint32_t need = (n + 15u) / 16u;
-        uint32_t g = (uint32_t)(di.cus * wps);
-        if (g > need) g = need;
-        hipLaunchKernelGGL((update_rows_pipe_kernel<6, 2, 16, 1>), dim3(g), dim3(kBlock), 0, stream,
-                           arena, arena_bytes, desc, n, base16, status, patch);
-        break;
-    }
-#define NFCS_FLAT(K, M)                                                                           \
-    hipLaunchKernelGGL((update_flat_kernel<K, M, 0>), dim3((n + 4u * M - 1u) / (4u * M)), dim3(kBlock), \
-                       0, stream, arena, arena_bytes, desc, n, base16, status, patch)
-    case 44: NFCS_FLAT(6, 4); break;
-    case 45: NFCS_FLAT(6, 5); break;
-    case 46: NFCS_FLAT(6, 6); break;
-    case 48: NFCS_FLAT(8, 8); break;
-    case 43: NFCS_FLAT(6, 3); break;
-#undef NFCS_FLAT
-    case 40: hipLaunchKernelGGL((update_win_kernel<6, 16, 64, 0, 6>), dim3((n + 255u) / 256u),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch); break;  // window mode (flat stream per wave), K=6
-    case 41: hipLaunchKernelGGL((update_win_kernel<6, 16, 64, 0, 8>), dim3((n + 255u) / 256u),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch); break;  // window mode, 8 slots per flat step
-    case 20: NFCS_LP(6, 16, 0, patch); break;  // v4: lane plans, 16-lane row sums
-    case 21: NFCS_LP(6, 8, 0, patch); break;   // v4: lane plans, 8-lane row sums
-    case 22:
-    case 23: {  // v4 split: checksum pass without frame stores, then the patch pass
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        if (variant == 22) NFCS_LP(6, 16, 1, pp);
-        else NFCS_LP(6, 8, 1, pp);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
-    }
-    case 101: NFCS_ROWSP(6, 2, 16, 1, patch); break;  // no frame stores
-    case 102: NFCS_ROWSP(6, 2, 16, 2, patch); break;  // no parse (fixed C1 plan)
-    case 103: NFCS_ROWSP(6, 2, 16, 3, patch); break;  // neither
-    case 105: NFCS_ROWSP(12, 2, 8, 1, patch); break;  // 8-lane rows, no frame stores
-    case 106: NFCS_ROWSP(12, 2, 8, 3, patch); break;  // 8-lane rows, no stores, no parse
-    case 131: NFCS_ROWSO(6, 2, 16, 0, 6, patch); break;  // >= 6 waves per SIMD
-    case 141: NFCS_ROWSP(6, 2, 16, 4, patch); break;  // high priority compute phase
-    case 142: NFCS_ROWSP(6, 2, 16, 8, patch); break;  // high priority load issue
-    case 155: NFCS_ROWS(12, 1, 8); break;      // 8-lane rows, all loads evict-first
-    case 156: NFCS_ROWS(8, 2, 8); break;       // 8-lane rows, 8 slots
-    case 157: NFCS_ROWS(6, 2, 8); break;       // 8-lane rows, 6 slots (768 B per batch)
-    case 158: NFCS_ROWS(4, 2, 8); break;       // 8-lane rows, 4 slots
-    case 159: NFCS_ROWSP(6, 2, 8, 1, patch); break;  // 8-lane rows, 6 slots, no frame stores
+#ifdef NFCS_EXPERIMENTS  // ablations and alternatives, measurement builds (libnfcs_exp.so) only
+#include "nfcs_update_variants.inc"
 #endif
     }
 #undef NFCS_LP
