@@ -1,0 +1,96 @@
+"""The C ABI's error convention on a GPU (include/nfcs.h): where the reference's
+void members return silently, every entry point here returns NFCS_OK or a negative NFCS_E* code
+and never touches memory on a rejected call; per-packet problems (a descriptor outside the arena)
+are status bytes, not call failures. Called straight through ctypes, as a foreign binding would."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import netflow_amd as nf
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+OK, EINVAL = 0, -1
+
+
+def _frames(n=64):
+    return oracle.fuzz_frames(515, 0, n)
+
+
+def test_null_and_empty_arguments(engine):
+    L = nf.lib()
+    d = engine.alloc(4096)
+    assert L.nfcs_update_device(None, d.ptr, 4096, d.ptr, 1, None, None, None) == EINVAL
+    assert L.nfcs_update_device(engine.ctx, None, 4096, d.ptr, 1, None, None, None) == EINVAL
+    assert L.nfcs_update_device(engine.ctx, d.ptr, 4096, None, 1, None, None, None) == EINVAL
+    # n = 0 is a no-op whatever the pointers
+    assert L.nfcs_update_device(engine.ctx, None, 0, None, 0, None, None, None) == OK
+    assert L.nfcs_flow_keys_device(engine.ctx, None, 0, None, 0, None, None, None) == OK
+    assert L.nfcs_l3_forward_device(engine.ctx, None, 0, None, None, 0, None, 0, None, None) == OK
+    assert L.nfcs_vlan_device(engine.ctx, None, 0, None, 0, None, 0, None, 0, None, None) == OK
+
+
+def test_misaligned_pointers_are_rejected_untouched(engine):
+    L = nf.lib()
+    arena, desc = oracle.pack_frames(_frames())
+    d_arena = engine.alloc(arena.nbytes + 64).upload(np.concatenate([arena, np.zeros(64, np.uint8)]))
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    n = len(desc)
+    before = d_arena.download(np.uint8, arena.nbytes + 64)
+    # arena not 16-byte aligned
+    assert L.nfcs_update_device(engine.ctx, d_arena.ptr + 8, arena.nbytes, d_desc.ptr, n, None, None, None) == EINVAL
+    assert L.nfcs_vlan_device(engine.ctx, d_arena.ptr + 4, arena.nbytes, d_desc.ptr, n, None,
+                              nf.VLAN_POP, None, 64, None, None) == EINVAL
+    # flow-key records must be 16-byte aligned
+    d_keys = engine.alloc(64 * n + 16)
+    assert L.nfcs_flow_keys_device(engine.ctx, d_arena.ptr, arena.nbytes, d_desc.ptr, n,
+                                   d_keys.ptr + 4, None, None) == EINVAL
+    # a next-hop table promised but missing
+    d_nh = engine.alloc(4 * n)
+    assert L.nfcs_l3_forward_device(engine.ctx, d_arena.ptr, arena.nbytes, d_desc.ptr, d_nh.ptr, n,
+                                    None, 3, None, None) == EINVAL
+    engine.sync()
+    assert np.array_equal(d_arena.download(np.uint8, arena.nbytes + 64), before)
+
+
+def test_host_path_argument_rules(engine):
+    L = nf.lib()
+    arena, desc = oracle.pack_frames(_frames())
+    n = len(desc)
+    rev = np.ascontiguousarray(desc[::-1])  # nfcs_update_host takes frames in arena order
+    before = arena.copy()
+    assert L.nfcs_update_host(engine.ctx, arena.ctypes.data, arena.nbytes, rev.ctypes.data, n, None, 0) == EINVAL
+    # zero-copy needs a pinned arena; this one is pageable
+    assert L.nfcs_update_host(engine.ctx, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n, None,
+                              nf.HOST_ZERO_COPY) == EINVAL
+    assert np.array_equal(arena, before)
+
+
+def test_descriptor_outside_the_arena_is_a_status_not_an_error(engine):
+    frames = _frames()
+    arena, desc = oracle.pack_frames(frames)
+    desc = desc.copy()
+    desc[3]["off16"] = arena.nbytes // 16 + 1          # starts past the arena
+    desc[5]["len"] = arena.nbytes                      # runs past the arena
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc)
+    d_arena = engine.alloc(arena.nbytes).upload(arena)
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_st = engine.alloc(len(desc))
+    engine.update_device(d_arena, arena.nbytes, d_desc, len(desc), d_st)  # raises on rc != 0
+    engine.sync()
+    st = d_st.download(np.uint8, len(desc))
+    assert st[3] == nf.ST_BAD_DESC and st[5] == nf.ST_BAD_DESC
+    assert np.array_equal(st, rst)
+    assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
+
+
+def test_strerror_covers_every_code():
+    L = nf.lib()
+    for rc in (0, -1, -2, -3, -4):
+        msg = L.nfcs_strerror(rc)
+        assert isinstance(msg, bytes) and len(msg) > 0
+    assert L.nfcs_abi_version() == 1
+    assert isinstance(ctypes.c_int(L.nfcs_last_hip_error()).value, int)
