@@ -94,3 +94,31 @@ def test_strerror_covers_every_code():
         assert isinstance(msg, bytes) and len(msg) > 0
     assert L.nfcs_abi_version() == 1
     assert isinstance(ctypes.c_int(L.nfcs_last_hip_error()).value, int)
+
+
+def test_contexts_on_threads_are_independent():
+    """One context per host thread on the same device (the documented threading model): four
+    threads update their own batches concurrently, each bit-exact with the oracle."""
+    import threading
+    results = {}
+
+    def work(t):
+        frames = oracle.fuzz_frames(700 + t, 0, 20000)
+        arena, desc = oracle.pack_frames(frames)
+        ref = arena.copy()
+        rst, _ = oracle.update_batch(ref, desc)
+        with nf.Engine(0) as e:
+            d_arena = e.alloc(arena.nbytes).upload(arena)
+            d_desc = e.alloc(desc.nbytes).upload(desc)
+            d_st = e.alloc(len(desc))
+            e.update_device(d_arena, arena.nbytes, d_desc, len(desc), d_st)
+            e.sync()
+            results[t] = (bool(np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)),
+                          bool(np.array_equal(d_st.download(np.uint8, len(desc)), rst)))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert results == {t: (True, True) for t in range(4)}
