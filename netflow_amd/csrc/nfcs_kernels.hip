@@ -625,6 +625,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //    65536 / 131072  patch records stored nt / write-through
 //  2097152 / 4194304  XCD order in chunks of 64 / 8 blocks   8388608  dispatch order (no remap)
 // 16777216  slots past every row's frame not issued (wave-uniform branches)
+// 33554432 / 67108864  checksum stores `sc1 nt` / `sc0`
 // Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
 // wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
@@ -793,6 +794,12 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                 else if (DBG & 4096) {
                     const uint32_t bv = b;
                     asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(frame + pos), "v"(bv) : "memory");
+                } else if (DBG & 33554432) {  // sc1 nt
+                    const uint32_t bv = b;
+                    asm volatile("global_store_byte %0, %1, off sc1 nt" ::"v"(frame + pos), "v"(bv) : "memory");
+                } else if (DBG & 67108864) {  // sc0 (workgroup-scope write-through)
+                    const uint32_t bv = b;
+                    asm volatile("global_store_byte %0, %1, off sc0" ::"v"(frame + pos), "v"(bv) : "memory");
                 } else {
                     st8<!(DBG & 8192)>(frame + pos, b);
                 }
