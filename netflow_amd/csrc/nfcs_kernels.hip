@@ -626,6 +626,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //  2097152 / 4194304  XCD order in chunks of 64 / 8 blocks   8388608  dispatch order (no remap)
 // 16777216  slots past every row's frame not issued (wave-uniform branches)
 // 33554432 / 67108864  checksum stores `sc1 nt` / `sc0`
+// 134217728 / 268435456  first wave of each workgroup touches the arena 8 / 32 MiB ahead
 // Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
 // wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
@@ -1002,6 +1003,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
         T[7] = ((uint64_t)xcc << 32) | hw;
     }
     DescW<PW> Dn = load_descw<PW>(desc, w0, n);
+    // measurement (DBG 134217728 / 268435456): the workgroup's first wave touches one dword of
+    // the arena 8 / 32 MiB past its first frame, so that page's translation is walked before
+    // the stream reaches it (batches whose footprint exceeds ~2 GB run slower per byte)
+    uint32_t tp = 0;
+    if ((DBG & (134217728 | 268435456)) && arena_bytes >= 64u) {
+        constexpr uint64_t AH = (DBG & 134217728) ? (8ull << 20) : (32ull << 20);
+        uint64_t a = (uint64_t)(Dn.w[0] - base16) * 16u + AH;
+        if (a > arena_bytes - 64u) a = arena_bytes - 64u;
+        uint32_t z = 0;
+        asm volatile("" : "+v"(z));
+        if (threadIdx.x == 0) tp = __builtin_nontemporal_load((const uint32_t*)(arena + a) + z);
+    }
     if (DBG & 256) T[1] = ts_now();  // the wave's descriptors have landed
     uint32_t Qn[PW];
     if (FWD && !(DBG & 16)) load_nh(Qn, w0);
@@ -1039,6 +1052,7 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
         row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac, T);
     }
     if (DBG & 192) asm volatile("" ::"v"(pf));  // keeps the prefetch load
+    if (DBG & (134217728 | 268435456)) asm volatile("" ::"v"(tp));  // keeps the page touch
     if (DBG & 256) {  // the frame stores acknowledged; the wave's stamps go to `patch`
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         T[5] = ts_now();

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -71,8 +72,9 @@ float run(const uint4* p, size_t n16, int grid, unsigned long long* o) {
     return best;
 }
 
-int main() {
-    const size_t bytes = 1504ull * 1048576ull;  // the C1 arena size
+int main(int argc, char** argv) {
+    // default: the C1 arena size; argv[1] = frames in units of 1M x 1504 B (4 = the C4 shard)
+    const size_t bytes = 1504ull * 1048576ull * (argc > 1 ? (size_t)atoi(argv[1]) : 1);
     uint4* p; unsigned long long* o;
     hipMalloc(&p, bytes); hipMalloc(&o, 8); hipMemset(p, 1, bytes);
     hipDeviceProp_t prop; hipGetDeviceProperties(&prop, 0);
@@ -84,7 +86,7 @@ int main() {
         printf("{\"grid\": %d, \"u1_GBs\": %.1f, \"u4_GBs\": %.1f, \"u4_nt_GBs\": %.1f}\n", g,
                bytes / t1 / 1e6, bytes / t4 / 1e6, bytes / t4n / 1e6);
     }
-    uint2* side; hipMalloc(&side, 1048576 * 8);
+    uint2* side; hipMalloc(&side, bytes / 1504 * 8);
     for (int g : grids) {
         float r0 = run_rw<0>(p, n16, side, g, o), r1 = run_rw<1>(p, n16, side, g, o), r2 = run_rw<2>(p, n16, side, g, o);
         printf("{\"grid\": %d, \"read_GBs\": %.1f, \"read+inplace4B_GBs\": %.1f, \"read+side8B_GBs\": %.1f}\n", g,
