@@ -49,6 +49,11 @@ constexpr uint64_t kSplitMeanBytes = 2048;
 // frames make short-lived waves, and single-wave workgroups retire and relaunch them with less
 // granularity loss (C3 +2-3%, profiles/r01_s2_variants.md run bs1/bs2).
 constexpr uint64_t kSmallMeanBytes = 1200;
+// At or above this arena size the C1-form kernel stores its checksum bytes write-back instead
+// of write-through: over a batch too large to stay partly cached between launches (the C4
+// shard, 6.3 GB) write-back measured 0.657 vs 0.632; re-processing a 1.5 GB batch, write-through
+// 0.765 vs 0.743 (profiles/r01_s4_batch_footprint.jsonl).
+constexpr uint64_t kWriteBackArenaBytes = 2ull << 30;
 inline bool use_split(int variant, uint64_t arena_bytes, uint32_t n) {
     return variant == 8 || (variant >= 9 && variant <= 14) || variant == 22 ||
            variant == 23 ||  // 9-14, 22, 23: experiments build only

@@ -612,8 +612,8 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     if (FWD) __builtin_amdgcn_sched_barrier(0);
 }
 
-// DBG bits of update_rows_kernel. The product instantiates DBG 0 (and 1 for split mode's first
-// pass); every other value exists only in measurement builds (NFCS_EXPERIMENTS, variants in
+// DBG bits of update_rows_kernel. The product instantiates DBG 0, 1 for split mode's first
+// pass and 8192 for arenas of at least kWriteBackArenaBytes; every other value exists only in measurement builds (NFCS_EXPERIMENTS, variants in
 // launch_update / launch_l3_forward; results in profiles/r01_s2_variants.md):
 //        1  no frame stores (split mode's first pass writes patch records only)
 //        2  fixed C1 plan, no parse                  4 / 8  s_setprio 3 over compute / load issue
@@ -1109,6 +1109,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     if (n == 0) return hipSuccess;
     if (variant == 0 && use_split(0, arena_bytes, n)) variant = 8;  // large frames: split mode
     if (variant == 0 && arena_bytes / n < kSmallMeanBytes) variant = 29;  // short frames: 1-wave WGs
+    if (variant == 0 && arena_bytes >= kWriteBackArenaBytes) variant = 30;  // large batch: write-back
     // One workgroup per 4*64/R packets, as many workgroups as that takes (a grid that
     // grid-strides over resident workgroups measured 10-15% slower: DESIGN.md §5).
     auto rows_grid = [&](int R) {
@@ -1137,6 +1138,11 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 64>), dim3((n + 3u) / 4u),
                            dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
                            nofwd);
+        break;
+    case 30:  // as 0 with plain (write-back) checksum stores, for arenas >= kWriteBackArenaBytes
+        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 1, false, 1>), dim3(rows_grid(16)),
+                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
+                           patch, nofwd);
         break;
     case 8: {  // split: checksum pass without frame stores, then the patch pass (plain stores:
                // a write-through patch pass measured C2 0.805 vs 0.823, variant 9)
