@@ -627,6 +627,8 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 // 16777216  slots past every row's frame not issued (wave-uniform branches)
 // 33554432 / 67108864  checksum stores `sc1 nt` / `sc0`
 // 134217728 / 268435456  first wave of each workgroup touches the arena 8 / 32 MiB ahead
+// 536870912  with 16384: the segment store covers the frame's whole first 128-byte line
+//            (262144: its first 64 bytes); with 8192 as well the segment is stored write-back
 // Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
 // wait for every scalar load issued before it.
 DEV uint64_t ts_now() {
@@ -844,7 +846,8 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                 }
             }
             if (DBG & 262144) last = max(last, 3u);  // measurement: a whole 64-byte half line
-            if (any && rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
+            if (DBG & 536870912) last = max(last, 7u);  // measurement: the whole 128-byte line
+            if (any && rl <= last && 16u * rl < len) st16<!(DBG & 8192)>((uint4*)frame + rl, v);
         }
         emit(S.valid && !slow, st, ipw, l4w, false);
     } else {
