@@ -1,0 +1,68 @@
+"""The write-back store form of the checksum kernel (variant 30), which `nfcs_update_device`
+chooses for arenas of at least 2 GiB (kWriteBackArenaBytes), against the oracle
+and the reference: (a) forced on a fresh fuzz batch, byte for byte, status and patch records;
+(b) chosen by size on BASELINE C4 shards (4M x 1500 B = 6.3 GB), whose whole-arena digests must
+equal the reference's (tests/golden/configs.json, made from the compiled reference)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import netflow_amd as nf
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture
+def wb_engine(monkeypatch):
+    monkeypatch.setenv("NFCS_VARIANT", "30")  # read by nfcs_ctx_create
+    e = nf.Engine(0)
+    yield e
+    e.close()
+
+
+def test_write_back_form_fuzz_vs_oracle(wb_engine):
+    frames = oracle.fuzz_frames(30, 0, 60000)
+    for align in (16, 128):
+        arena, desc = oracle.pack_frames(frames, align=align)
+        ref = arena.copy()
+        rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+        n = len(desc)
+        d_arena = wb_engine.alloc(arena.nbytes).upload(arena)
+        d_desc = wb_engine.alloc(desc.nbytes).upload(desc)
+        d_st = wb_engine.alloc(n)
+        d_pt = wb_engine.alloc(8 * n)
+        wb_engine.update_device(d_arena, arena.nbytes, d_desc, n, d_st, d_pt)
+        wb_engine.sync()
+        assert np.array_equal(d_st.download(np.uint8, n), rst)
+        assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
+        pt = d_pt.download(nf.PATCH_DTYPE, n)
+        re = arena.copy()  # the patch records reproduce the update on the original frames
+        for i in range(n):
+            o = int(desc[i]["off16"]) * 16
+            for f in ("ip", "l4"):
+                if pt[i][f + "_off"] != 0xFFFF:
+                    re[o + int(pt[i][f + "_off"]): o + int(pt[i][f + "_off"]) + 2] = pt[i][f]
+        assert np.array_equal(re, ref)
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c4_shard_digest_large_arena(engine, rank):
+    g = json.load(open(os.path.join(GOLD, "configs.json")))
+    sh = g["c4_rank_shards"][rank]
+    n = sh["n"]
+    d_arena, nbytes, d_desc, _ = engine.config_batch(1, g["seed"], sh["first"], n, 128)
+    assert nbytes >= 2 << 30  # the size that selects the write-back form
+    assert f"{engine.digest_device(d_arena, nbytes, d_desc, n, sh['first']):016x}" == sh["digest_in"]
+    engine.update_device(d_arena, nbytes, d_desc, n)
+    engine.sync()
+    dout = engine.digest_device(d_arena, nbytes, d_desc, n, sh["first"])
+    assert f"{dout:016x}" == sh["digest_out"]
+    engine.update_device(d_arena, nbytes, d_desc, n)  # idempotent
+    engine.sync()
+    assert engine.digest_device(d_arena, nbytes, d_desc, n, sh["first"]) == dout
+    d_arena.free()
+    d_desc.free()
