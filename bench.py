@@ -44,6 +44,7 @@ STREAM_READ_GBPS = 7007.0  # best read-only stream (nt loads)
 STREAM_RW_GBPS = 4839.0    # best read stream with one in-place store per 1536-byte frame
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 C4_PACKETS_PER_GPU = 1 << 22
+C4_SHARD_1GPU_GBPS = 5218.8  # bench.py --packets 4194304 on one MI355X, session 4
 WORKLOAD = {
     0: "C0: 1024 x 64 B IPv4 (header checksum only)",
     1: "C1: 1M x 1500 B IPv4+UDP, device-resident",
@@ -446,6 +447,13 @@ def main():
                                  "frac_of_read_only": round(achieved / STREAM_READ_GBPS, 4),
                                  "read_plus_one_store_per_frame_GBps": STREAM_RW_GBPS,
                                  "source": "profiles/r01_stream_microbench.md"}
+    if c4:
+        # the same 4M-packet shard on ONE GPU (profiles/r01_s4_bench_c4_shard_1gpu.json): the
+        # per-GPU rate this line scales, lower than the N = 1 (C1, 1M-packet) line because a
+        # 6.3 GB batch does not stay partly cached between launches
+        out["one_gpu_same_shard"] = {"value": C4_SHARD_1GPU_GBPS, "unit": "GB/s",
+                                     "linear_at_n": round(C4_SHARD_1GPU_GBPS * ws, 1),
+                                     "source": "profiles/r01_s4_bench_c4_shard_1gpu.json"}
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
