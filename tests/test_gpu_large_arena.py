@@ -2,7 +2,8 @@
 chooses for arenas of at least 2 GiB (kWriteBackArenaBytes), against the oracle
 and the reference: (a) forced on a fresh fuzz batch, byte for byte, status and patch records;
 (b) chosen by size on BASELINE C4 shards (4M x 1500 B = 6.3 GB), whose whole-arena digests must
-equal the reference's (tests/golden/configs.json, made from the compiled reference)."""
+equal the reference's (tests/golden/configs.json, made from the compiled reference). Also split
+mode (variant 8) forced on fuzz frames."""
 import json
 import os
 
@@ -66,3 +67,30 @@ def test_c4_shard_digest_large_arena(engine, rank):
     assert engine.digest_device(d_arena, nbytes, d_desc, n, sh["first"]) == dout
     d_arena.free()
     d_desc.free()
+
+
+def test_split_mode_fuzz_vs_oracle(monkeypatch):
+    """Split mode forced on fuzz frames (variant 8: the product's form for large frames, chosen
+    by size only for C2-like batches, so the fuzz corpus never reaches it on its own), byte for
+    byte against the oracle over two successive calls."""
+    monkeypatch.setenv("NFCS_VARIANT", "8")
+    e = nf.Engine(0)
+    try:
+        frames = oracle.fuzz_frames(8, 0, 60000)
+        for align in (16, 128):
+            arena, desc = oracle.pack_frames(frames, align=align)
+            n = len(desc)
+            d_arena = e.alloc(arena.nbytes).upload(arena)
+            d_desc = e.alloc(desc.nbytes).upload(desc)
+            d_st = e.alloc(n)
+            ref = arena.copy()
+            # the second call runs over the updated frames; the oracle follows the same sequence (frames with IHL < 5 overlaps
+            # change status on a second pass, in the reference as well)
+            for _ in range(2):
+                rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+                e.update_device(d_arena, arena.nbytes, d_desc, n, d_st)
+                e.sync()
+                assert np.array_equal(d_st.download(np.uint8, n), rst)
+                assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
+    finally:
+        e.close()
