@@ -44,7 +44,9 @@ STREAM_READ_GBPS = 7007.0  # best read-only stream (nt loads)
 STREAM_RW_GBPS = 4839.0    # best read stream with one in-place store per 1536-byte frame
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 C4_PACKETS_PER_GPU = 1 << 22
-C4_SHARD_1GPU_GBPS = 5218.8  # bench.py --packets 4194304 on one MI355X, session 4
+# bench.py --packets 4194304 on one MI355X, session 4: 5218.8 / 5399.6 / 5424.6 GB/s on three
+# boxes (profiles/r01_s4_bench_c4_shard_1gpu*.json); the median
+C4_SHARD_1GPU_GBPS = 5399.6
 WORKLOAD = {
     0: "C0: 1024 x 64 B IPv4 (header checksum only)",
     1: "C1: 1M x 1500 B IPv4+UDP, device-resident",
