@@ -613,8 +613,9 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 }
 
 // DBG bits of update_rows_kernel. The product instantiates DBG 0, 1 for split mode's first
-// pass and 8192 for arenas of at least kWriteBackArenaBytes; every other value exists only in measurement builds (NFCS_EXPERIMENTS, variants in
-// launch_update / launch_l3_forward; results in profiles/r01_s2_variants.md):
+// pass and 8192 for arenas of at least kWriteBackArenaBytes; every other value exists only in
+// measurement builds (NFCS_EXPERIMENTS, variants in launch_update / launch_l3_forward; results
+// in profiles/r01_s2_variants.md and r01_s4_batch_footprint.jsonl):
 //        1  no frame stores (split mode's first pass writes patch records only)
 //        2  fixed C1 plan, no parse                  4 / 8  s_setprio 3 over compute / load issue
 //       16  L3 forward: no next-hop index loads      64 / 128  descriptor prefetch 16k / 64k ahead
