@@ -94,3 +94,18 @@ def test_split_mode_fuzz_vs_oracle(monkeypatch):
                 assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
     finally:
         e.close()
+
+
+def test_zero_copy_large_pinned_arena(engine):
+    """nfcs_update_host zero-copy over a pinned host arena of more than 2 GiB (1.4M C1 frames,
+    128-byte aligned, 2.15 GB): the size rule picks the write-back form for a kernel whose frames
+    live in host memory; statuses and every byte against the oracle."""
+    n = 1_400_000
+    src, desc = oracle.gen_config(1, 20250620, 0, n, 128)
+    assert src.nbytes >= 2 << 30 and src.nbytes // n < 2048  # write-back form, not split mode
+    pinned = engine.host_array(src.nbytes)
+    pinned[:] = src
+    rst, _ = oracle.update_batch(src, desc, nthreads=8)
+    st = engine.update_host(pinned, desc, mode="zero_copy")
+    assert np.array_equal(st, rst)
+    assert np.array_equal(pinned, src)
