@@ -53,17 +53,12 @@ class NfcsError(RuntimeError):
     pass
 
 
-def build(verbose: bool = False, experiments: bool = False, out: str | None = None,
-          extra_flags: tuple = ()) -> str:
-    """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree).
-    experiments=True builds netflow_amd/libnfcs_exp.so with the measurement-only ablation
-    variants (NFCS_VARIANT >= 100); the product never loads it unless NFCS_LIB points at it.
-    out / extra_flags: measurement builds under another name with other compiler flags."""
-    if out is None:
-        out = os.path.join(HERE, "libnfcs_exp.so") if experiments else os.path.join(HERE, "libnfcs.so")
+def build(verbose: bool = False) -> str:
+    """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree). The measurement
+    build (extra launch forms for A/B runs) is separate: tools/exp/build.sh."""
+    out = os.path.join(HERE, "libnfcs.so")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"),
-           *(["-DNFCS_EXPERIMENTS"] if experiments else []), *extra_flags, *SOURCES, "-o", out]
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"), *SOURCES, "-o", out]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -188,12 +183,16 @@ class Engine:
 
     def __init__(self, device: int = 0):
         self.device = device
+        self._pinned = {}  # address -> size of the host_array() allocations still held
         c = _vp()
         _check(lib().nfcs_ctx_create(device, ctypes.byref(c)), f"nfcs_ctx_create({device})")
         self.ctx = c.value
 
     def close(self):
         if getattr(self, "ctx", None):
+            for p in list(self._pinned):
+                lib().nfcs_host_free(self.ctx, p)
+            self._pinned.clear()
             lib().nfcs_ctx_destroy(self.ctx)
             self.ctx = None
 
@@ -211,10 +210,20 @@ class Engine:
         return DeviceBuffer(self, nbytes)
 
     def host_array(self, nbytes: int) -> np.ndarray:
-        """A pinned host uint8 array (nfcs_host_alloc), freed with the engine's context."""
+        """A pinned host uint8 array (nfcs_host_alloc). Release it with host_free(); whatever is
+        still held when the engine closes is freed then (do not use such arrays afterwards)."""
         p = _vp()
-        _check(lib().nfcs_host_alloc(self.ctx, max(int(nbytes), 16), ctypes.byref(p)), "host_alloc")
-        return np.ctypeslib.as_array((ctypes.c_uint8 * max(int(nbytes), 16)).from_address(p.value))[:nbytes]
+        size = max(int(nbytes), 16)
+        _check(lib().nfcs_host_alloc(self.ctx, size, ctypes.byref(p)), "host_alloc")
+        self._pinned[p.value] = size
+        return np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p.value))[:nbytes]
+
+    def host_free(self, arr: np.ndarray):
+        """Free a host_array() allocation now (the array must not be used afterwards)."""
+        p = arr.__array_interface__["data"][0]
+        if self._pinned.pop(p, None) is None:
+            raise NfcsError("host_free: not a live host_array of this engine")
+        _check(lib().nfcs_host_free(self.ctx, p), "host_free")
 
     def sync(self, stream=None):
         _check(lib().nfcs_stream_sync(self.ctx, stream), "stream_sync")

@@ -20,6 +20,7 @@ struct nfcs_ctx {
     hipStream_t stream = nullptr;
     // host pipeline (nfcs_update_host)
     static constexpr int kSlots = 2;
+    static constexpr size_t kStageBytes = size_t(64) << 20;  // arena bytes per staging slot
     hipStream_t hs[kSlots] = {nullptr, nullptr};
     hipEvent_t done[kSlots] = {nullptr, nullptr};
     size_t stage_bytes = 0;   // arena bytes per slot
@@ -35,38 +36,46 @@ struct nfcs_ctx {
     nfcs_patch* h_patch[kSlots] = {nullptr, nullptr};
     uint64_t* d_digest = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int variant = 0;
-    int grid = 0;
-    nfcs_patch* ws = nullptr;  // split-mode patch workspace (grown on demand)
-    size_t ws_cap = 0;         // records
-    nfcs::Work work(size_t) {
-        nfcs::Work w;
-        w.patch = ws;
-        return w;
-    }
+    // patch records of the waves that defer their stores (kUpdateAuto without a caller d_patch),
+    // grown on demand; ws_ev marks the last launch that used it, on ws_stream
+    nfcs_patch* ws = nullptr;
+    size_t ws_cap = 0;  // records
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_used = false;
 };
 
 namespace {
 
 thread_local int g_last_hip = 0;
 
-hipError_t ensure_ws(nfcs_ctx* c, size_t n, uint64_t arena_bytes) {
-    if (!nfcs::variant_needs_ws(c->variant, arena_bytes, (uint32_t)n) || n <= c->ws_cap)
-        return hipSuccess;
-    if (c->ws) (void)hipFree(c->ws);
-    c->ws = nullptr;
-    c->ws_cap = 0;
-    size_t cap = n < (1u << 20) ? (1u << 20) : n;
-    hipError_t e = hipMalloc(&c->ws, cap * sizeof(nfcs_patch));
-    if (e == hipSuccess) c->ws_cap = cap;
-    return e;
+// The deferred-store workspace for a launch of n packets on `st`. A launch on another stream
+// than the previous user first waits (on the device) for that user's write pass, so calls on one
+// context from several streams never overwrite each other's records; growing it waits on the host.
+hipError_t acquire_ws(nfcs_ctx* c, size_t n, hipStream_t st) {
+    if (n > c->ws_cap) {
+        if (c->ws_used) {
+            hipError_t e = hipEventSynchronize(c->ws_ev);
+            if (e != hipSuccess) return e;
+        }
+        if (c->ws) (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_cap = 0;
+        c->ws_used = false;
+        const size_t cap = n < (1u << 20) ? (1u << 20) : n;
+        hipError_t e = hipMalloc(&c->ws, cap * sizeof(nfcs_patch));
+        if (e != hipSuccess) return e;
+        c->ws_cap = cap;
+    } else if (c->ws_used && c->ws_stream != st) {
+        hipError_t e = hipStreamWaitEvent(st, c->ws_ev, 0);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
-
-// host pipeline slot s: its own patch buffer as split workspace
-nfcs::Work host_work(nfcs_ctx* c, int s) {
-    nfcs::Work w;
-    w.patch = c->d_patch[s];
-    return w;
+hipError_t release_ws(nfcs_ctx* c, hipStream_t st) {
+    c->ws_stream = st;
+    c->ws_used = true;
+    return hipEventRecord(c->ws_ev, st);
 }
 
 int hip_fail(hipError_t e) {
@@ -80,11 +89,6 @@ int hip_fail(hipError_t e) {
     } while (0)
 
 hipStream_t pick(nfcs_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
-
-int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
 
 // memcpy split across threads: one host thread copies pageable memory at ~15-25 GB/s, below
 // what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned).
@@ -108,8 +112,8 @@ void par_memcpy(void* dst, const void* src, size_t bytes, int threads) {
 
 int ensure_host_pipeline(nfcs_ctx* ctx) {
     if (ctx->d_arena[0]) return NFCS_OK;
-    ctx->copy_threads = env_int("NFCS_COPY_THREADS", 8);
-    ctx->stage_bytes = (size_t)env_int("NFCS_STAGE_MB", 64) << 20;
+    ctx->copy_threads = 8;
+    ctx->stage_bytes = nfcs_ctx::kStageBytes;
     ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         NFCS_HIP(hipStreamCreateWithFlags(&ctx->hs[s], hipStreamNonBlocking));
@@ -139,46 +143,64 @@ bool is_pinned(const void* p) {
 
 // Pinned host arena: the kernel reads the frames over PCIe where they are and writes the 2+2
 // checksum bytes straight back (host memory from hipHostMalloc is mapped into the GPU's address
-// space). Only descriptors (8 B/packet) go H2D and statuses (1 B/packet) D2H, in chunks on the
-// two pipeline streams; frames cross the link once, in one direction.
+// space), inline from the read pass (kUpdateInline: a deferred write pass would cross the link
+// again). Only descriptors (8 B/packet) go H2D and statuses (1 B/packet) D2H, in chunks on the
+// two pipeline streams; frames cross the link once, in one direction. On an error both slots are
+// drained before returning, so nothing is left in flight on the caller's memory.
 int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
                           const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status) {
     void* dptr = nullptr;
     NFCS_HIP(hipHostGetDevicePointer(&dptr, h_arena, 0));
     uint8_t* d_arena = static_cast<uint8_t*>(dptr);
     uint32_t cnt[nfcs_ctx::kSlots] = {0, 0}, first[nfcs_ctx::kSlots] = {0, 0};
-    auto finish = [&](int s) -> int {
-        if (!cnt[s]) return NFCS_OK;
-        NFCS_HIP(hipEventSynchronize(c->done[s]));
-        if (h_status) memcpy(h_status + first[s], c->h_status[s], cnt[s]);
+    hipError_t e = hipSuccess;
+    // wait for slot s; its statuses are copied out only while no error has occurred
+    auto finish = [&](int s) {
+        if (!cnt[s]) return;
+        const hipError_t f = hipEventSynchronize(c->done[s]);
+        if (e == hipSuccess) e = f;
+        if (e == hipSuccess && h_status) memcpy(h_status + first[s], c->h_status[s], cnt[s]);
         cnt[s] = 0;
-        return NFCS_OK;
     };
     int s = 0;
-    for (uint32_t i = 0; i < n; s ^= 1) {
-        int rc = finish(s);
-        if (rc) return rc;
+    for (uint32_t i = 0; i < n && e == hipSuccess; s ^= 1) {
+        finish(s);
+        if (e != hipSuccess) break;
         const uint32_t m = std::min<uint32_t>(n - i, c->stage_pkts);
         hipStream_t st = c->hs[s];
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
-        NFCS_HIP(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
-                                hipMemcpyHostToDevice, st));
-        NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, c->d_desc[s], m, 0u,
-                                     h_status ? c->d_status[s] : nullptr, nullptr, st,
-                                     // fused kernel: a separate patch pass buys nothing
-                                     // when the stores go over PCIe anyway
-                                     (c->variant == 0 || c->variant == 8) ? 24 : c->variant,
-                                     c->grid, nfcs::Work{}));
-        if (h_status)
-            NFCS_HIP(hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st));
-        NFCS_HIP(hipEventRecord(c->done[s], st));
+        e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
+                           hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = nfcs::launch_update(c->di, d_arena, arena_bytes, c->d_desc[s], m, 0u,
+                                    h_status ? c->d_status[s] : nullptr, nullptr, nullptr,
+                                    nfcs::kUpdateInline, st);
+        if (e == hipSuccess && h_status)
+            e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);  // whatever was queued on this slot has finished
+            break;
+        }
         first[s] = i;
         cnt[s] = m;
         i += m;
     }
-    int rc = finish(s);
-    if (rc) return rc;
-    return finish(s ^ 1);
+    finish(s);  // drain both slots, also after an error
+    finish(s ^ 1);
+    if (e != hipSuccess) return hip_fail(e);
+    return NFCS_OK;
+}
+
+// The device-resident update on stream st: kUpdateAuto, deferred records into the caller's
+// d_patch when given, else into the context workspace.
+int update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfcs_desc* d_desc,
+                  uint32_t n, uint8_t* d_status, nfcs_patch* d_patch, hipStream_t st) {
+    if (!d_patch) NFCS_HIP(acquire_ws(c, n, st));
+    NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0u, d_status, d_patch,
+                                 d_patch ? nullptr : c->ws, nfcs::kUpdateAuto, st));
+    if (!d_patch) NFCS_HIP(release_ws(c, st));
+    return NFCS_OK;
 }
 
 }  // namespace
@@ -217,11 +239,9 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     c->di.device = device;
     c->di.cus = prop.multiProcessorCount;
     strncpy(c->di.arch, prop.gcnArchName, sizeof(c->di.arch) - 1);
-    c->variant = env_int("NFCS_VARIANT", 0);
-    c->di.lds_pad = (unsigned)env_int("NFCS_LDS_PAD", 0);
-    c->grid = env_int("NFCS_GRID", 0);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_digest, sizeof(uint64_t));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
@@ -250,6 +270,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     }
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -265,10 +286,7 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
     if (!c) return NFCS_EINVAL;
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
-    NFCS_HIP(ensure_ws(c, n, arena_bytes));
-    NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, d_patch,
-                                 pick(c, stream), c->variant, c->grid, c->work(n)));
-    return NFCS_OK;
+    return update_device(c, d_arena, arena_bytes, d_desc, n, d_status, d_patch, pick(c, stream));
 }
 
 NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
@@ -280,7 +298,7 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
     if (!d_arena || !d_desc || !d_nh || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (table_n > 0 && (!d_table || ((uintptr_t)d_table & 3u))) return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
-                                     d_status, pick(c, stream), c->grid, c->variant));
+                                     d_status, pick(c, stream)));
     return NFCS_OK;
 }
 
@@ -293,7 +311,7 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
-                               cap_all, d_status, pick(c, stream), c->variant));
+                               cap_all, d_status, pick(c, stream)));
     return NFCS_OK;
 }
 
@@ -305,7 +323,7 @@ NFCS_API int nfcs_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u) || ((uintptr_t)d_keys & 15u))
         return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash,
-                                    pick(c, stream), c->variant));
+                                    pick(c, stream)));
     return NFCS_OK;
 }
 
@@ -315,34 +333,49 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     if (!c) return NFCS_EINVAL;
     if (n == 0) return NFCS_OK;
     if (!h_arena || !h_desc) return NFCS_EINVAL;
-    for (uint32_t i = 1; i < n; ++i)
-        if (h_desc[i].off16 < h_desc[i - 1].off16) return NFCS_EINVAL;  // must be arena order
+    // Checked before anything is queued: frames in arena order, and every frame that lies inside
+    // the arena fits one staging slot. A frame reaching past the arena is staged as nothing and
+    // becomes NFCS_ST_BAD_DESC (the kernel checks it against its chunk), as on the device path.
+    auto frame_end = [&](uint32_t i) -> uint64_t {  // 0: outside the arena
+        const uint64_t o = (uint64_t)h_desc[i].off16 * 16u;
+        const uint64_t e = o + (((uint64_t)h_desc[i].len + 15u) & ~15ull);
+        return e <= arena_bytes ? e : 0;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+        if (i && h_desc[i].off16 < h_desc[i - 1].off16) return NFCS_EINVAL;
+        const uint64_t e = frame_end(i);
+        if (e && e - (uint64_t)h_desc[i].off16 * 16u > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
+    }
     int rc = ensure_host_pipeline(c);
     if (rc) return rc;
-    // default: frames H2D, 8-byte patch records D2H, applied here (measured fastest); whole
-    // frames back only on request (NFCS_HOST_FRAMES)
-    const bool patch_only = !(flags & NFCS_HOST_FRAMES);
     const bool pinned = is_pinned(h_arena);
     if (flags & NFCS_HOST_ZERO_COPY) {
         if (!pinned) return NFCS_EINVAL;
         return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status);
     }
+    // default: frames H2D and only the 8-byte patch records D2H (kUpdateRecords: the staged
+    // frames are not written), applied here; whole frames back only on request (NFCS_HOST_FRAMES:
+    // kUpdateAuto on the staged frames, the slot's patch buffer as the deferred-store workspace)
+    const bool patch_only = !(flags & NFCS_HOST_FRAMES);
 
     struct Chunk { uint32_t i0, i1; uint64_t base, bytes; bool used; };
     Chunk slot[nfcs_ctx::kSlots] = {};
-
-    // finish a slot: wait for its D2H, then copy frames / apply patches / copy statuses
-    auto finish = [&](int s) -> int {
+    hipError_t e = hipSuccess;
+    // finish a slot: wait for its D2H, then apply patches / copy frames / copy statuses (only
+    // while no error has occurred; after one the slot is only drained)
+    auto finish = [&](int s) {
         Chunk& k = slot[s];
-        if (!k.used) return NFCS_OK;
-        NFCS_HIP(hipEventSynchronize(c->done[s]));
+        if (!k.used) return;
+        k.used = false;
+        const hipError_t f = hipEventSynchronize(c->done[s]);
+        if (e == hipSuccess) e = f;
+        if (e != hipSuccess) return;
         const uint32_t m = k.i1 - k.i0;
         if (patch_only) {
             for (uint32_t i = 0; i < m; ++i) {
                 const nfcs_patch& pt = c->h_patch[s][i];
-                const uint64_t off = (uint64_t)h_desc[k.i0 + i].off16 * 16u;
-                if (off + h_desc[k.i0 + i].len > arena_bytes) continue;
-                uint8_t* f = h_arena + off;
+                if (!frame_end(k.i0 + i)) continue;
+                uint8_t* f = h_arena + (uint64_t)h_desc[k.i0 + i].off16 * 16u;
                 if (pt.ip_off != NFCS_PATCH_NONE) { f[pt.ip_off] = pt.ip[0]; f[pt.ip_off + 1] = pt.ip[1]; }
                 if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
             }
@@ -350,64 +383,65 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             par_memcpy(h_arena + k.base, c->h_arena[s], k.bytes, c->copy_threads);
         }
         if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
-        k.used = false;
-        return NFCS_OK;
     };
 
     uint32_t i = 0;
     int s = 0;
-    while (i < n) {
-        // next chunk: packets [i0, i1) whose frames fit one staging slot
-        const uint64_t base = (uint64_t)h_desc[i].off16 * 16u;
+    while (i < n && e == hipSuccess) {
+        // next chunk: packets [i, i1) whose in-arena frames fit one staging slot
+        const uint64_t base = std::min<uint64_t>((uint64_t)h_desc[i].off16 * 16u, arena_bytes);
         uint32_t i1 = i;
         uint64_t end = base;
         while (i1 < n && i1 - i < c->stage_pkts) {
-            const uint64_t o = (uint64_t)h_desc[i1].off16 * 16u;
-            const uint64_t e = std::min<uint64_t>(o + (((uint64_t)h_desc[i1].len + 15u) & ~15ull),
-                                                  arena_bytes);
-            const uint64_t ne = std::max(end, e);
-            if (ne - base > c->stage_bytes) {
-                if (i1 == i) return NFCS_EINVAL;  // a single frame larger than a slot
-                break;
-            }
+            const uint64_t fe = frame_end(i1);
+            const uint64_t ne = std::max(end, fe);
+            if (ne - base > c->stage_bytes) break;  // i1 > i: a single frame always fits (above)
             end = ne;
             ++i1;
         }
-        rc = finish(s);
-        if (rc) return rc;
-        Chunk& k = slot[s];
-        k = {i, i1, base, end - base, true};
+        finish(s);
+        if (e != hipSuccess) break;
         const uint32_t m = i1 - i;
+        const uint64_t bytes = end - base;
         const uint8_t* src = h_arena + base;
         if (!pinned) {
-            par_memcpy(c->h_arena[s], src, k.bytes, c->copy_threads);
+            par_memcpy(c->h_arena[s], src, bytes, c->copy_threads);
             src = c->h_arena[s];
         }
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
         hipStream_t st = c->hs[s];
-        NFCS_HIP(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
-                                hipMemcpyHostToDevice, st));
-        NFCS_HIP(hipMemcpyAsync(c->d_arena[s], src, k.bytes, hipMemcpyHostToDevice, st));
-        NFCS_HIP(nfcs::launch_update(c->di, c->d_arena[s], k.bytes, c->d_desc[s], m,
-                                     (uint32_t)(base >> 4), c->d_status[s],
-                                     patch_only ? c->d_patch[s] : nullptr, st, c->variant,
-                                     c->grid, host_work(c, s)));
-        if (patch_only) {
-            NFCS_HIP(hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
-                                    hipMemcpyDeviceToHost, st));
-        } else {
-            uint8_t* dst = pinned ? h_arena + base : c->h_arena[s];
-            NFCS_HIP(hipMemcpyAsync(dst, c->d_arena[s], k.bytes, hipMemcpyDeviceToHost, st));
+        e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
+                           hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && bytes)
+            e = hipMemcpyAsync(c->d_arena[s], src, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = nfcs::launch_update(c->di, c->d_arena[s], bytes, c->d_desc[s], m, (uint32_t)(base >> 4),
+                                    c->d_status[s], patch_only ? c->d_patch[s] : nullptr,
+                                    patch_only ? nullptr : c->d_patch[s],
+                                    patch_only ? nfcs::kUpdateRecords : nfcs::kUpdateAuto, st);
+        if (e == hipSuccess) {
+            if (patch_only)
+                e = hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
+                                   hipMemcpyDeviceToHost, st);
+            else if (bytes)
+                e = hipMemcpyAsync(pinned ? h_arena + base : c->h_arena[s], c->d_arena[s], bytes,
+                                   hipMemcpyDeviceToHost, st);
         }
-        if (h_status)
-            NFCS_HIP(hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st));
-        NFCS_HIP(hipEventRecord(c->done[s], st));
+        if (e == hipSuccess && h_status)
+            e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);  // whatever was queued on this slot has finished
+            break;
+        }
+        slot[s] = {i, i1, base, bytes, true};
         i = i1;
         s ^= 1;
     }
-    rc = finish(s);
-    if (rc) return rc;
-    return finish(s ^ 1);
+    finish(s);  // drain both slots, also after an error
+    finish(s ^ 1);
+    if (e != hipSuccess) return hip_fail(e);
+    return NFCS_OK;
 }
 
 NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
@@ -495,31 +529,18 @@ NFCS_API int nfcs_stream_sync(nfcs_ctx* c, void* stream) {
     return NFCS_OK;
 }
 
-#ifdef NFCS_EXPERIMENTS
-// Measurement build only: one launch of a timeline variant (90-93) with 8 u64 per wave of
-// 16-lane rows written to d_ts (tools/wave_timeline.py).
-NFCS_API int nfcs_exp_wave_timeline(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
-                                    const nfcs_desc* d_desc, uint32_t n, int variant,
-                                    uint64_t* d_ts) {
-    if (!c || !d_ts || variant < 90 || variant > 93) return NFCS_EINVAL;
-    hipStream_t st = pick(c, nullptr);
-    NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, nullptr,
-                                 (nfcs_patch*)d_ts, st, variant, c->grid, c->work(n)));
-    NFCS_HIP(hipStreamSynchronize(st));
-    return NFCS_OK;
-}
-#endif
 
 NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0) return NFCS_EINVAL;
     hipStream_t st = pick(c, stream);
-    NFCS_HIP(ensure_ws(c, n, arena_bytes));
+    if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     NFCS_HIP(hipEventRecord(c->ev0, st));
-    for (int it = 0; it < iters; ++it)
-        NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0, d_status, nullptr,
-                                     st, c->variant, c->grid, c->work(n)));
+    for (int it = 0; it < iters; ++it) {
+        const int rc = update_device(c, d_arena, arena_bytes, d_desc, n, d_status, nullptr, st);
+        if (rc) return rc;
+    }
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -535,7 +556,7 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
-                                         table_n, d_status, st, c->grid, c->variant));
+                                         table_n, d_status, st));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -551,8 +572,7 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
-                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
-                                   c->variant));
+                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -566,8 +586,7 @@ NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uin
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
-        NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st,
-                                        c->variant));
+        NFCS_HIP(nfcs::launch_flow_keys(c->di, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

@@ -497,9 +497,6 @@ DEV uint4 ld16(const uint4* p) {
 // frame's line, so the line leaves as a clean eviction and the write goes to memory at once
 // instead of as a later write-back in the middle of the read stream (session 3: C1 +2.5%,
 // C3 +5% over plain stores; `sc0 sc1` measured the same, `sc0 sc1 nt` 5% worse).
-DEV void st16_nt(uint4* p, const uint4& v) {
-    __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)p);
-}
 
 template <bool WT>
 DEV void st8(uint8_t* p, uint32_t b) {
@@ -577,10 +574,13 @@ struct FwdArgs {
     uint32_t table_n;
 };
 
-template <int K, int NT, int R = 16, bool FWD = false, bool SKIP = false>
+// Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
+// parsed and, with inline stores, written back while still in L2), payload slots non-temporal
+// (evict-first). Every load is always issued — lanes past the frame read g_zero16 — so the waits
+// are counted vmcnt waits.
+template <int K, int R = 16, bool FWD = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0,
-                   const FwdArgs* fa = nullptr) {
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     const bool bad = valid && ((d.off16 < base16) ||
@@ -594,17 +594,11 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
-    // every load always issued (lanes past the frame read g_zero16): counted vmcnt waits
-    // (SKIP, measurement: slots past every row's frame in the wave are not issued at all)
-    const uint32_t wmax = SKIP ? wave_max_rows<R>(nch) : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k;
         const uint4* a = (c < nch) ? src + c : &g_zero16;
-        // NT 2: the header slot keeps the default policy so its lines are still in L2 when
-        // the checksum chunks are written back; payload slots stream through as evict-first
-        if (SKIP && k > 0 && (uint32_t)R * k >= wmax) S.v[k] = make_uint4(0u, 0u, 0u, 0u);
-        else S.v[k] = (NT == 2 && k == 0) ? ld16<0>(a) : ld16<NT>(a);
+        S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
     }
     // all K loads issue before any use of the header slot: without this fence the scheduler
     // hoists the forward decision's first DPP read above the last loads of the FWD kernel and
@@ -612,46 +606,30 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     if (FWD) __builtin_amdgcn_sched_barrier(0);
 }
 
-// DBG bits of update_rows_kernel. The product instantiates DBG 0, 1 for split mode's first
-// pass and 8192 for arenas of at least kWriteBackArenaBytes; every other value exists only in
-// measurement builds (NFCS_EXPERIMENTS, variants in launch_update / launch_l3_forward; results
-// in profiles/r01_s2_variants.md and r01_s4_batch_footprint.jsonl):
-//        1  no frame stores (split mode's first pass writes patch records only)
-//        2  fixed C1 plan, no parse                  4 / 8  s_setprio 3 over compute / load issue
-//       16  L3 forward: no next-hop index loads      64 / 128  descriptor prefetch 16k / 64k ahead
-//      256  per-wave timeline stamps into `patch`    512 / 1024 / 4096  nt / sc0 sc1 / sc0 sc1 nt
-//     8192  plain (write-back) frame stores               checksum stores
-//    16384  one write-through segment store per packet (the L3 forward's default form)
-//    32768  L3 forward: 16-byte + byte stores instead of the segment store
-//    65536 / 131072  patch records stored nt / write-through
-//  2097152 / 4194304  XCD order in chunks of 64 / 8 blocks   8388608  dispatch order (no remap)
-// 16777216  slots past every row's frame not issued (wave-uniform branches)
-// 33554432 / 67108864  checksum stores `sc1 nt` / `sc0`
-// 134217728 / 268435456  first wave of each workgroup touches the arena 8 / 32 MiB ahead
-// 536870912  with 16384: the segment store covers the frame's whole first 128-byte line
-//            (262144: its first 64 bytes); with 8192 as well the segment is stored write-back
-// Timeline stamps: s_memtime returns the shader clock; the trailing lgkmcnt(0) makes the stamp
-// wait for every scalar load issued before it.
-DEV uint64_t ts_now() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
+// How update_rows_kernel's checksum bytes reach the frames:
+//   SF_INLINE   the row's lanes 0-3 store the 2+2 bytes write-through (sc1) as soon as they are
+//               known: one 64-byte write request per packet inside the read stream;
+//   SF_DEFER    per wave, from its four descriptor lengths (SGPRs): a wave whose frames average
+//               at least kDeferMeanBytes writes 8-byte patch records instead, and
+//               apply_bytes_kernel writes them after the read pass with non-temporal stores (the
+//               writes then reach HBM in a write-only pass instead of interleaving with, or being
+//               evicted from the memory-side cache into, the read stream); other waves as SF_INLINE;
+//   SF_RECORDS  patch records only, frames untouched (nfcs_update_host: only the records cross
+//               PCIe back).
+enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
 
-template <int K, int NT, int DBG = 0, int R = 16, bool FWD = false, int SV = 0>
+// SF_DEFER's decision for the P packets pw .. pw+P-1 (lengths 0 past n), shared by the read pass
+// and apply_bytes_kernel so both pick the same waves.
+DEV bool defer_group(uint32_t lensum, uint32_t P) { return lensum >= P * (uint32_t)kDeferMeanBytes; }
+DEV uint32_t defer_len(uint32_t len) { return len < 0xFFFFu ? len : 0xFFFFu; }
+
+template <int K, int R = 16, bool FWD = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
-                     nfcs_patch* patch, uint32_t table_n = 0, const uint32_t* wmac = nullptr,
-                     uint64_t* T = nullptr) {
-    if (DBG & 256) {  // the header slot (first of the K loads) has landed
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K - 1) : "memory");
-        T[2] = ts_now();
-    }
+                     nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
+                     const uint32_t* wmac = nullptr) {
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
-    if (DBG & 4) __builtin_amdgcn_s_setprio(3);  // finish the compute phase first
     const bool live = S.valid && !S.bad;
     uint4 h0 = S.v[0];
     // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
@@ -688,13 +666,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             else h0.y -= 1u << 16;
         }
     }
-    RPlan P;
-    if (DBG & 2) {
-        P = rplan_none(NFCS_ST_V4_UDP);
-        P.flags = F_IP | F_L4 | F_UDP; P.ipw = 24; P.rs = 34; P.re = len; P.fs = 40; P.corr = 0;
-    } else {
-        P = fast_plan<R>(h0, rowbase4, len);
-    }
+    RPlan P = fast_plan<R>(h0, rowbase4, len);
     const bool act = live && (!FWD || fwd);  // rows whose checksums are updated
     // uncommon headers (IP options, IHL < 5, IHL past the frame) take the cold path below,
     // after the chunk registers are dead, so it adds nothing to the kernel's register peak
@@ -702,26 +674,22 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     if (!act || slow)
         P = rplan_none(S.bad ? (uint32_t)NFCS_ST_BAD_DESC
                              : (FWD && live && !fwd) ? fst : (uint32_t)NFCS_ST_NONE);
-    uint32_t st = P.st | ((FWD && fwd) ? (uint32_t)NFCS_ST_FLAG_FWD : 0u);
-    uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
+    const uint32_t st = P.st | ((FWD && fwd) ? (uint32_t)NFCS_ST_FLAG_FWD : 0u);
+    const uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
     uint32_t l4w = NFCS_PATCH_NONE;
-    // region sums (rows without an L4 region add nothing). rlv is opaque so the per-slot
-    // offsets are recomputed rather than hoisted into ~35 long-lived VGPRs.
+    // Region sums without per-slot boundary branches (rows without an L4 region add nothing):
+    // chunks below nre are added whole (the region starts below byte 80, in slot 0, where
+    // dwords under lo4 are masked); the last chunk's bytes past re and the odd trailing byte
+    // are corrected once per row by the lane that holds it. Frames longer than one batch leave
+    // their end to the masked continuation below. rlv is opaque so the per-slot offsets are
+    // recomputed rather than hoisted into ~35 long-lived VGPRs.
     const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
     const uint32_t tailfix = P.flags & F_TAIL;
     uint32_t rlv = rl;
     asm volatile("" : "+v"(rlv));
     uint32_t acc = 0;
     const uint32_t nre = (re + 15u) >> 4;
-    if (SV == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc_slot(acc, k == 0 ? h0 : S.v[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
-    } else {
-        // Sums without per-slot boundary branches: chunks below nre are added whole (the
-        // region starts below byte 80, in slot 0, where dwords under lo4 are masked); the last
-        // chunk's bytes past re and the odd trailing byte are corrected once per row by the
-        // lane that holds it. Frames longer than one batch leave their end to the masked
-        // continuation below.
+    {
         const uint32_t last = nre - 1u, own = (re != 0) && (last < (uint32_t)R * K) && ((last & (R - 1)) == rl);
         uint4 lc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -760,10 +728,6 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             if (tailfix) acc += 255u * ((comp(lc, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
         }
     }
-    if (DBG & 256) {  // every slot has landed and been summed
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        T[3] = ts_now();
-    }
     // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t cmax = wave_max_rows<R>(nre);
     for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
@@ -771,7 +735,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = cb + rlv + (uint32_t)R * k;
-            w[k] = ld16<NT>((c < nre) ? src + c : &g_zero16);
+            w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k, lo4, re, tailfix);
@@ -782,100 +746,57 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         if ((P.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
         l4w = P.fs | (c << 16);
     }
-    // Write back the (at most 4) checksum bytes from lanes 0..3 of the row (byte stores
-    // measured fastest: chunk, dword, whole-line and re-load-then-store write-backs all
-    // slower), then the status byte / patch record from lane 0.
-    auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool frame_stores) {
-        if (!(DBG & 1) && frame_stores && on && rl < 4) {
+    // The (at most 4) checksum bytes from lanes 0..3 of the row, write-through (sc1: the L2
+    // keeps no dirty copy of the header line; session 3, C1 +2.5% / C3 +5% over write-back
+    // stores; byte stores measured fastest against chunk, dword, whole-line and re-load-then-
+    // store forms), then the status byte / patch record from lane 0.
+    auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool stores) {
+        if (stores && on && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w_ : ipw_;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) {
-                const uint8_t b = (uint8_t)(w >> (16 + 8 * (rl & 1u)));
-                // measurement builds: 512 nt, 1024 system scope (sc0 sc1), 4096 sc0 sc1 nt,
-                // 8192 plain (write-back) stores; default write-through (sc1)
-                if (DBG & 512) __builtin_nontemporal_store(b, frame + pos);
-                else if (DBG & 1024) __hip_atomic_store(frame + pos, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                else if (DBG & 4096) {
-                    const uint32_t bv = b;
-                    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(frame + pos), "v"(bv) : "memory");
-                } else if (DBG & 33554432) {  // sc1 nt
-                    const uint32_t bv = b;
-                    asm volatile("global_store_byte %0, %1, off sc1 nt" ::"v"(frame + pos), "v"(bv) : "memory");
-                } else if (DBG & 67108864) {  // sc0 (workgroup-scope write-through)
-                    const uint32_t bv = b;
-                    asm volatile("global_store_byte %0, %1, off sc0" ::"v"(frame + pos), "v"(bv) : "memory");
-                } else {
-                    st8<!(DBG & 8192)>(frame + pos, b);
-                }
-            }
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<true>(frame + pos, w >> (16 + 8 * (rl & 1u)));
         }
         if (on && rl == 0) {
             if (status) status[S.p] = (uint8_t)st_;
-            if (patch) {
+            if (rec) {
                 uint2 r;
                 r.x = (ipw_ & 0xFFFFu) | (l4w_ << 16);
                 r.y = (ipw_ >> 16) | (l4w_ & 0xFFFF0000u);
-                uint2* q = (uint2*)patch + S.p;
-                if (DBG & 65536) __builtin_nontemporal_store(((uint64_t)r.y << 32) | r.x, (uint64_t*)q);
-                else if (DBG & 131072)
-                    __hip_atomic_store((uint64_t*)q, ((uint64_t)r.y << 32) | r.x, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                else *q = r;
+                ((uint2*)rec)[S.p] = r;
             }
         }
     };
-    // Segment stores (the fused forward; DBG 16384 for the plain update, measured no faster
-    // there): one write-through segment per packet. Lanes 0..c store chunks 0..c of the header
-    // (c = the last chunk holding a byte to write) from the header registers with the checksum
-    // bytes and the forward's rewrite patched in; unchanged bytes are rewritten with the values
-    // just read from them (a frame never shares a 16-byte chunk with another frame). L3 forward
-    // +1.5% over a 16-byte store + byte stores (variant 119).
-    constexpr bool SEG = (FWD && !(DBG & 32768)) || (DBG & 16384);
-    if (SEG) {
-        if (!(DBG & 1) && S.valid && !slow) {
+    if (FWD) {
+        // The fused forward's segment store: one write-through segment per forwarded packet.
+        // Lanes 0..c store chunks 0..c of the header (c = the last chunk holding a byte to
+        // write) from the header registers with the checksum bytes and the forward's rewrite
+        // patched in; unchanged bytes are rewritten with the values just read from them (a frame
+        // never shares a 16-byte chunk with another frame). +1.5% over a 16-byte store + byte
+        // stores (session 3).
+        if (S.valid && !slow && fwd) {
             uint4 v = h0;
-            uint32_t last = (FWD && fwd) ? 1u : 0u;
-            bool any = FWD && fwd;
+            uint32_t last = 1u;
 #pragma unroll
             for (uint32_t t = 0; t < 4; ++t) {
                 const uint32_t w = (t < 2) ? ipw : l4w;
                 const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
                 if ((w & 0xFFFFu) != NFCS_PATCH_NONE) {
-                    any = true;
                     last = max(last, pos >> 4);
                     if ((pos >> 4) == rl) v = put_byte(v, pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
                 }
             }
-            if (DBG & 262144) last = max(last, 3u);  // measurement: a whole 64-byte half line
-            if (DBG & 536870912) last = max(last, 7u);  // measurement: the whole 128-byte line
-            if (any && rl <= last && 16u * rl < len) st16<!(DBG & 8192)>((uint4*)frame + rl, v);
+            if (rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
         }
         emit(S.valid && !slow, st, ipw, l4w, false);
     } else {
-        // the rewritten header bytes, beside the checksum bytes (one write transaction per
-        // line; storing them before the sums measured 0.5% slower) and before the cold path
-        // reads them
-        if (FWD && fwd && !(DBG & 1)) {
-            if (rl == 0) st16<!(DBG & 8192)>((uint4*)frame, h0);  // len >= 34: chunk 0 is the frame's own
-            if (rl == 1) st8<!(DBG & 8192)>(frame + (tagged ? 26 : 22), ttl - 1u);
-        }
-        emit(S.valid && !slow && !(DBG & 256), st, ipw, l4w, true);
+        emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
-    if (DBG & 256) {  // frame stores issued; status / patch are not written in this mode
-        if (!(DBG & 1) && S.valid && !slow && rl < 4) {
-            const uint32_t w = (rl & 2u) ? l4w : ipw;
-            const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<!(DBG & 8192)>(frame + pos, w >> (16 + 8 * (rl & 1u)));
-        }
-        T[4] = ts_now();
-    }
-    if (DBG & 4) __builtin_amdgcn_s_setprio(0);
     if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
         // Uncommon headers, handled last so that only the frame address and length are live
         // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
         // exact sequential emulation, which writes its own bytes) and the region is re-summed
         // from memory.
-        if (FWD && SEG && !(DBG & 1) && slow && fwd) {
+        if (FWD && slow && fwd) {
             // segment stores skip uncommon headers: their forward rewrite goes out here, from
             // the next-hop MACs (SGPRs) and the TTL byte in memory (the header registers are
             // dead by now, which keeps the fast path free of spills)
@@ -932,52 +853,44 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             l4w2 = ol4;
         }
         if (FWD) st2 |= NFCS_ST_FLAG_FWD;
-        emit(slow, st2, ipw2, l4w2, !seq);
+        // the forward always stores (its header rewrite went out above)
+        emit(slow, st2, ipw2, l4w2, !seq && (FWD || frame_stores));
     }
 }
 
-// Grid-stride over packets (the default grid has one workgroup per 4*64/R packets, so no
-// loop), 64/R packet rows per wave.
-template <int K, int NT, int R = 16, int DBG = 0, int OCC = 1, bool FWD = false, int SV = 0,
-          int BS = kBlock>
+// One wave = 64/R packet rows; one workgroup per BS/R packets, as many workgroups as the batch
+// needs (a grid that strides over resident workgroups measured 10-15% slower).
+// XCD-aware block order (session 3): workgroups are dealt to the 8 XCDs round-robin; remapped,
+// the workgroups one XCD runs take one contiguous eighth of the batch, so each XCD streams its
+// own region of HBM and the descriptor lines its workgroups share stay in its L2 (a bijection on
+// [0, gridDim.x); the tail beyond a multiple of 8 keeps its order). C1 +1.3%, C3 +0.5%.
+template <int K, int R, int OCC, int BS, bool FWD, int SF>
 __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
-                                                                  uint64_t arena_bytes,
-                                                                  const nfcs_desc* __restrict__ desc,
-                                                                  uint32_t n, uint32_t base16,
-                                                                  uint8_t* __restrict__ status,
-                                                                  nfcs_patch* __restrict__ patch,
-                                                                  FwdArgs fa) {
+                                                              uint64_t arena_bytes,
+                                                              const nfcs_desc* __restrict__ desc,
+                                                              uint32_t n, uint32_t base16,
+                                                              uint8_t* __restrict__ status,
+                                                              nfcs_patch* __restrict__ patch,
+                                                              nfcs_patch* __restrict__ ws,
+                                                              FwdArgs fa) {
     constexpr uint32_t PW = 64 / R;  // packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint32_t stride = gridDim.x * (BS / R);
-    // XCD-aware block order (session 3): workgroups are dealt to the 8 XCDs round-robin;
-    // remapped, the workgroups one XCD runs take one contiguous eighth of the batch, so each
-    // XCD streams its own region of HBM and the descriptor lines its workgroups share stay in
-    // its L2 (a bijection on [0, gridDim.x); the tail beyond a multiple of 8 keeps its order).
-    // C1 +1.3%, C3 +0.5%, measured (variants 129/128 at the time; DBG 8388608 turns it off).
-    uint32_t bid = blockIdx.x;
-    if (!(DBG & (8388608 | 2097152 | 4194304))) {
-        const uint32_t g8 = gridDim.x / 8u;
-        if (bid < 8u * g8) bid = (bid % 8u) * g8 + bid / 8u;
-    } else if (DBG & (2097152 | 4194304)) {  // measurement: chunks of C blocks dealt round-robin
-        constexpr uint32_t C = (DBG & 2097152) ? 64u : 8u;
-        const uint32_t full = gridDim.x / (8u * C) * (8u * C);
-        if (bid < full) {
-            const uint32_t x = bid % 8u, k = bid / 8u;
-            bid = ((k / C) * 8u + x) * C + k % C;
-        }
-    }
-    const uint64_t w0 = (uint64_t)bid * (BS / R) + rfl(threadIdx.x >> 6) * PW;
-    if (w0 >= n) return;
+    const uint64_t pw = (uint64_t)xcd_block() * (BS / R) + rfl(threadIdx.x >> 6) * PW;
+    if (pw >= n) return;
+    // the wave's PW descriptors: one scalar load (s_load_dwordx8 for PW = 4)
+    const DescW<PW> D = load_descw<PW>(desc, pw, n);
     // Fused L3 forward: the wave's PW next-hop indexes and their table rows are wave-uniform.
     // Read through the constant address space they are scalar loads on lgkmcnt, issued with the
     // descriptors so both arrive in one round trip (as generic loads the compiler made each
     // index a vector load drained by vmcnt(0) ahead of the frame loads: four serial memory
     // round trips per wave).
     typedef const __attribute__((address_space(4))) uint32_t cu32;
-    auto load_nh = [&](uint32_t (&q)[PW], uint64_t pw) {
+    uint32_t nh = 0;
+    uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
+    if (FWD) {
         const cu32* nhp = (const cu32*)fa.nh + pw;
+        uint32_t q[PW];
         if (pw + PW <= n) {
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) q[i] = nhp[i];
@@ -985,221 +898,126 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
         }
-    };
-    // measurement (DBG 64 / 128): touch the descriptor line of the wave that starts ~one
-    // residency later, so its scalar descriptor load hits L2 instead of HBM
-    uint32_t pf = 0;
-    if (DBG & 192) {
-        constexpr uint64_t D = (DBG & 64) ? 16384u : 65536u;  // packets ahead
-        uint32_t z = 0;
-        asm volatile("" : "+v"(z));  // a vector load (a scalar one would be waited on at once)
-        if (lane == 0 && w0 + D < n) pf = ((const uint32_t*)(desc + w0 + D))[z];
-    }
-    uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (DBG & 256) {
-        uint64_t rt;
-        uint32_t hw, xcc;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        T[0] = ts_now();
-        T[6] = rt;
-        T[7] = ((uint64_t)xcc << 32) | hw;
-    }
-    DescW<PW> Dn = load_descw<PW>(desc, w0, n);
-    // measurement (DBG 134217728 / 268435456): the workgroup's first wave touches one dword of
-    // the arena 8 / 32 MiB past its first frame, so that page's translation is walked before
-    // the stream reaches it (batches whose footprint exceeds ~2 GB run slower per byte)
-    uint32_t tp = 0;
-    if ((DBG & (134217728 | 268435456)) && arena_bytes >= 64u) {
-        constexpr uint64_t AH = (DBG & 134217728) ? (8ull << 20) : (32ull << 20);
-        uint64_t a = (uint64_t)(Dn.w[0] - base16) * 16u + AH;
-        if (a > arena_bytes - 64u) a = arena_bytes - 64u;
-        uint32_t z = 0;
-        asm volatile("" : "+v"(z));
-        if (threadIdx.x == 0) tp = __builtin_nontemporal_load((const uint32_t*)(arena + a) + z);
-    }
-    if (DBG & 256) T[1] = ts_now();  // the wave's descriptors have landed
-    uint32_t Qn[PW];
-    if (FWD && !(DBG & 16)) load_nh(Qn, w0);
-    if (FWD && (DBG & 16)) {  // measurement: next hop 0 for every packet, no index loads
 #pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) Qn[i] = 0;
-    }
-    for (uint64_t pw = w0; pw < n; pw += stride) {
-        const DescW<PW> D = Dn;
-        uint32_t q[PW];
-#pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) q[i] = FWD ? Qn[i] : 0u;
-        if (pw + stride < n) {  // prefetch (lgkmcnt)
-            Dn = load_descw<PW>(desc, pw + stride, n);
-            if (FWD && !(DBG & 16)) load_nh(Qn, pw + stride);
+        for (uint32_t i = 0; i < PW; ++i) {
+            nh |= (row == i) ? q[i] : 0u;
+            const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i]) : (const cu32*)&g_zero16;
+            wmac[3 * i] = m[0];
+            wmac[3 * i + 1] = m[1];
+            wmac[3 * i + 2] = m[2];
         }
-        RowStage<K> S;
-        uint32_t nh = 0;
-        uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
-        if (FWD) {
-#pragma unroll
-            for (uint32_t i = 0; i < PW; ++i) {
-                nh |= (row == i) ? q[i] : 0u;
-                const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i])
-                                                    : (const cu32*)&g_zero16;
-                wmac[3 * i] = m[0];
-                wmac[3 * i + 1] = m[1];
-                wmac[3 * i + 2] = m[2];
-            }
-        }
-        if (DBG & 8) __builtin_amdgcn_s_setprio(3);  // issue the loads first
-        row_stage<K, NT, R, FWD, (DBG & 16777216) != 0>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16,
-                                 rl, nh, &fa);
-        if (DBG & 8) __builtin_amdgcn_s_setprio(0);
-        row_process<K, NT, DBG, R, FWD, SV>(S, rl, rowbase4, status, patch, fa.table_n, wmac, T);
     }
-    if (DBG & 192) asm volatile("" ::"v"(pf));  // keeps the prefetch load
-    if (DBG & (134217728 | 268435456)) asm volatile("" ::"v"(tp));  // keeps the page touch
-    if (DBG & 256) {  // the frame stores acknowledged; the wave's stamps go to `patch`
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        T[5] = ts_now();
-        if (lane < 8) {
-            uint64_t t = T[0];
+    // the wave's store form, from its own frame lengths (scalar arithmetic on the descriptors)
+    bool defer = false;
+    if (SF == SF_DEFER) {
+        uint32_t s = 0;
 #pragma unroll
-            for (uint32_t i = 1; i < 8; ++i) t = (lane == i) ? T[i] : t;
-            ((uint64_t*)patch)[(w0 / PW) * 8u + lane] = t;
+        for (uint32_t i = 0; i < PW; ++i) s += defer_len(D.w[2 * i + 1]);
+        defer = defer_group(s, PW);
+    }
+    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
+    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
+    RowStage<K> S;
+    row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, nh);
+    row_process<K, R, FWD>(S, rl, rowbase4, status, rec, frame_stores, fa.table_n, wmac);
+}
+
+// SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
+// with ONE store request per packet, non-temporal at system scope (`sc0 sc1 nt`): the writes go to
+// HBM during this write-only pass instead of lingering dirty in the memory-side cache and being
+// evicted into the next read stream (4M x 1500 B shard: read pass + this pass 0.715-0.718 of 8 TB/s
+// against 0.658 for the fused kernel with write-back stores; tools/wr_probe.hip).
+// One thread per packet: lane l of a wave loads descriptor p0 + l (one coalesced 512-byte load)
+// and, from the lengths of its aligned quad of lanes, recomputes the read pass's decision for that
+// group of 4 packets; only deferred packets load their record. The stores go out in 4 rounds of 16
+// packets: in round k lane l writes byte l % 4 of (ip[0], ip[1], l4[0], l4[1]) of packet 16k + l/4
+// (its record and frame offset by ds_bpermute), so the packet's 4 bytes leave in one store
+// instruction as one write request with a byte mask. An IPv4 byte that the L4 field overlaps
+// (IHL < 5) is left to the L4 lane: the reference writes the L4 field last.
+__global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict__ arena,
+                                                             const nfcs_desc* __restrict__ desc,
+                                                             uint32_t n, uint32_t base16,
+                                                             const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
+    uint32_t s = defer_len(d.len);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
+    const bool dfr = i < n && defer_group(s, 4);
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(dfr);
+    if (!mask) return;
+    uint2 r = make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
+    if (dfr) r = ((const uint2*)rec)[i];
+    const uint32_t j = lane & 3u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (((mask >> (16u * k)) & 0xFFFFu) == 0) continue;  // wave-uniform
+        const int q4 = (int)((16u * k + (lane >> 2)) * 4u);  // source lane, in bytes
+        const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.x);
+        const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.y);
+        const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d.off16);
+        const uint32_t ipo = rx & 0xFFFFu, l4o = rx >> 16;
+        const uint32_t off = j < 2 ? ipo : l4o;
+        const uint32_t a = off + (j & 1u);
+        const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+        if (off != NFCS_PATCH_NONE && !overlap) {
+            const uint32_t b = (j < 2 ? (ry >> (8 * j)) : (ry >> (16 + 8 * (j - 2)))) & 0xFFu;
+            uint8_t* p = arena + ((uint64_t)o16 - base16) * 16u + a;
+            asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");
         }
     }
 }
-
-// Split mode, second pass: write the patch records of the checksum pass into the frames. A
-// write-only pass over 8 bytes per packet, so the frame stream of the first pass carries no
-// scattered stores (each write transaction in a read stream costs far more than its bytes).
-template <bool WT>
-__global__ __launch_bounds__(kBlock) void apply_patches_kernel(uint8_t* __restrict__ arena,
-                                                               const nfcs_desc* __restrict__ desc,
-                                                               uint32_t n, uint32_t base16,
-                                                               const nfcs_patch* __restrict__ patch) {
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const uint2 r = ((const uint2*)patch)[i];
-        const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
-        if (ipo == NFCS_PATCH_NONE && l4o == NFCS_PATCH_NONE) continue;
-        uint8_t* f = arena + ((uint64_t)desc[i].off16 - base16) * 16u;
-        if (ipo != NFCS_PATCH_NONE) {  // l2 + 10: always even
-            if (WT) __hip_atomic_store((uint16_t*)(f + ipo), (uint16_t)(r.y & 0xFFFFu), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            else *(uint16_t*)(f + ipo) = (uint16_t)(r.y & 0xFFFFu);
-        }
-        if (l4o != NFCS_PATCH_NONE) {  // TCP's field at l4 + 15 is odd
-            if (l4o & 1u) {
-                st8<WT>(f + l4o, r.y >> 16);
-                st8<WT>(f + l4o + 1, r.y >> 24);
-            } else if (WT) {
-                __hip_atomic_store((uint16_t*)(f + l4o), (uint16_t)(r.y >> 16), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                *(uint16_t*)(f + l4o) = (uint16_t)(r.y >> 16);
-            }
-        }
-    }
-}
-
-#ifdef NFCS_EXPERIMENTS  // measured alternatives, measurement builds only
-#include "nfcs_experiments.inc"
-#endif  // NFCS_EXPERIMENTS
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, hipStream_t stream, int variant, int grid,
-                         const Work& work) {
-    nfcs_patch* ws = work.patch;
+                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream) {
+    (void)di;
     if (n == 0) return hipSuccess;
-    if (variant == 0 && use_split(0, arena_bytes, n)) variant = 8;  // large frames: split mode
-    if (variant == 0 && arena_bytes / n < kSmallMeanBytes) variant = 29;  // short frames: 1-wave WGs
-    if (variant == 0 && arena_bytes >= kWriteBackArenaBytes) variant = 30;  // large batch: write-back
-    // One workgroup per 4*64/R packets, as many workgroups as that takes (a grid that
-    // grid-strides over resident workgroups measured 10-15% slower: DESIGN.md §5).
-    auto rows_grid = [&](int R) {
-        const uint32_t per_block = (uint32_t)(kBlock / R);
-        const uint32_t need = (n + per_block - 1) / per_block;
-        return grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
-    };
+    if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
+    if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
     const FwdArgs nofwd = {nullptr, nullptr, 0};
-#define NFCS_ROWSO(K, NT, R, DBG, OCC, PP)                                                       \
-    hipLaunchKernelGGL((update_rows_kernel<K, NT, R, DBG, OCC>), dim3(rows_grid(R)), dim3(kBlock), \
-                       0, stream, arena, arena_bytes, desc, n, base16, status, PP, nofwd)
-#define NFCS_ROWSP(K, NT, R, DBG, PP) NFCS_ROWSO(K, NT, R, DBG, 1, PP)
-#define NFCS_ROWS(K, NT, R) NFCS_ROWSP(K, NT, R, 0, patch)
-#define NFCS_LP(K, R, DBG, PP)                                                                    \
-    hipLaunchKernelGGL((update_lp_kernel<K, R, 64, DBG>), dim3((n + 255u) / 256u), dim3(kBlock), 0, \
-                       stream, arena, arena_bytes, desc, n, base16, status, PP)
-    switch (variant) {
-    default:
-    case 0:  // 16-lane rows; header slot cached, payload evict-first; branch-free sums
-    case 24: hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 1, false, 1>), dim3(rows_grid(16)),
-                                dim3(kBlock), di.lds_pad, stream, arena, arena_bytes, desc, n, base16, status,
-                                patch, nofwd); break;
-    case 29:  // as 0 in one-wave workgroups (4 packets each): measured +2-3% on C3, -0.7% on C1;
-              // __launch_bounds__ 7 waves/SIMD caps the kernel at 94 SGPRs: at the compiler's 106
-              // the SGPR file (800 per SIMD, 16-register granule + 16) admits only 6 (C3 +2%)
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 0, 7, false, 1, 64>), dim3((n + 3u) / 4u),
-                           dim3(64), 0, stream, arena, arena_bytes, desc, n, base16, status, patch,
-                           nofwd);
-        break;
-    case 30:  // as 0 with plain (write-back) checksum stores, for arenas >= kWriteBackArenaBytes
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 8192, 1, false, 1>), dim3(rows_grid(16)),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status,
-                           patch, nofwd);
-        break;
-    case 8: {  // split: checksum pass without frame stores, then the patch pass (plain stores:
-               // a write-through patch pass measured C2 0.805 vs 0.823, variant 9)
-        nfcs_patch* pp = patch ? patch : ws;
-        if (!pp) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, 1, 1, false, 1>), dim3(rows_grid(16)),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, base16, status, pp,
-                           nofwd);
-        int ga = (int)((n + kBlock - 1) / kBlock);
-        if (ga > di.cus * 8) ga = di.cus * 8;
-        hipLaunchKernelGGL(apply_patches_kernel<false>, dim3(ga), dim3(kBlock), 0, stream, arena, desc, n,
-                           base16, pp);
-        break;
+    // Short frames (mean footprint under kSmallMeanBytes per packet) run in one-wave workgroups
+    // held at 7 waves/SIMD: short frames make short-lived waves, and single-wave workgroups retire
+    // and relaunch them with less granularity loss (C3 +2-3%); __launch_bounds__ 7 caps the kernel
+    // at 94 SGPRs (at the compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). The
+    // shape changes speed only: the store form is each wave's own (SF_DEFER).
+    // 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad bytes of (unused) LDS: at the
+    // 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768 vs 0.777, the 4M shard 0.710
+    // vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh); one-wave workgroups keep 8.
+    const bool small = arena_bytes / n < kSmallMeanBytes;
+    const dim3 g1((n + 3u) / 4u), g4((n + 15u) / 16u);
+#define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
+    hipLaunchKernelGGL((update_rows_kernel<6, 16, OCC, BS, false, SF>), G, dim3(BS),                \
+                       BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc, n, base16,  \
+                       status, patch, ws, nofwd)
+    if (form == kUpdateRecords) {
+        NFCS_ROWS(1, kBlock, g4, SF_RECORDS);
+    } else if (form == kUpdateInline) {
+        if (small) NFCS_ROWS(7, 64, g1, SF_INLINE);
+        else NFCS_ROWS(1, kBlock, g4, SF_INLINE);
+    } else {
+        if (small) NFCS_ROWS(7, 64, g1, SF_DEFER);
+        else NFCS_ROWS(1, kBlock, g4, SF_DEFER);
+        hipLaunchKernelGGL(apply_bytes_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                           arena, desc, n, base16, patch ? patch : ws);
     }
-#ifdef NFCS_EXPERIMENTS  // ablations and alternatives, measurement builds (libnfcs_exp.so) only
-#include "nfcs_update_variants.inc"
-#endif
-    }
-#undef NFCS_LP
 #undef NFCS_ROWS
-#undef NFCS_ROWSP
-#undef NFCS_ROWSO
     return hipGetLastError();
 }
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream, int grid, int variant) {
+                             hipStream_t stream) {
     (void)di;
     if (n == 0) return hipSuccess;
-    const uint32_t need = (n + 15u) / 16u;
-    const int g = grid > 0 ? (grid < (int)need ? grid : (int)need) : (int)need;
     const FwdArgs fa = {nh, table, table_n};
-#define NFCS_FWD(DBG, OCC, F)                                                                    \
-    hipLaunchKernelGGL((update_rows_kernel<6, 2, 16, DBG, OCC, F, 1>), dim3(g), dim3(kBlock), 0, \
-                       stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr, fa)
-    switch (variant) {
-#ifdef NFCS_EXPERIMENTS
-    // ablations (measurement build only): results differ from the reference on purpose
-    case 101: NFCS_FWD(1, 7, true); break;   // no frame stores
-    case 102: NFCS_FWD(0, 7, false); break;  // the plain update, same launch
-    case 103: NFCS_FWD(0, 1, true); break;   // no occupancy bound: 81 VGPRs, 6 waves per SIMD
-    case 116: NFCS_FWD(16, 7, true); break;  // no next-hop index loads (next hop 0)
-    case 118: NFCS_FWD(8192 | 32768, 7, true); break;  // plain (write-back) 16-B + byte stores
-    case 119: NFCS_FWD(32768, 7, true); break;         // write-through 16-B + byte stores
-
-#endif
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
-    // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower: variant 103)
-    default: NFCS_FWD(0, 7, true); break;
-    }
-#undef NFCS_FWD
+    // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
+    hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_INLINE>), dim3((n + 15u) / 16u),
+                       dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, 0u, status,
+                       (nfcs_patch*)nullptr, (nfcs_patch*)nullptr, fa);
     return hipGetLastError();
 }
 
@@ -1274,7 +1092,7 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K, int K2 = 2, bool WT = false, bool NTS = false, bool XR = false>
+template <int K, int K2 = 2, bool WT = false>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1287,7 +1105,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     constexpr uint32_t PW = 4, KR = (uint32_t)(K * R);
     const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
     const uint32_t rowbase4 = (lane & ~15u) * 4u;
-    const uint64_t pw = (uint64_t)(XR ? xcd_block() : blockIdx.x) * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
     const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
     uint32_t op = op_all, cap = cap_all;
@@ -1386,13 +1204,13 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst || (k == 0 && patched)) (NTS ? st16_nt((uint4*)frame + c, nv[k]) : st16<WT>((uint4*)frame + c, nv[k]));
+            if (c < nst || (k == 0 && patched)) st16<WT>((uint4*)frame + c, nv[k]);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst) (NTS ? st16_nt((uint4*)frame + c, nv[k]) : st16<WT>((uint4*)frame + c, nv[k]));
+            if (c < nst) st16<WT>((uint4*)frame + c, nv[k]);
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
         // the rest of a long frame in batches of K2 slots (K2 < K saves VGPRs: w and e live
@@ -1412,7 +1230,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
-                if (c < nst) (NTS ? st16_nt((uint4*)frame + c, e[k]) : st16<WT>((uint4*)frame + c, e[k]));
+                if (c < nst) st16<WT>((uint4*)frame + c, e[k]);
             }
         }
         l4w = finish(acc);
@@ -1473,29 +1291,16 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream, int variant) {
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream) {
+    (void)di;
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + 15u) / 16u;  // 4 rows per wave, 4 waves per workgroup
-    // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD). Batches of 2 slots
-    // (variant 31: 94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, and capping the
-    // occupancy lower with LDS padding slower still (profiles/r01_s2_occupancy.md).
-    if (variant == 31)
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 2, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
-                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
-#ifdef NFCS_EXPERIMENTS
-    else if (variant == 34)  // XCD-aware block order (measured 2% slower here: not adopted)
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, false, true>), dim3(blocks), dim3(kBlock), di.lds_pad,
-                           stream, arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
-    else if (variant == 33)  // non-temporal chunk stores (checksum bytes written through)
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, true>), dim3(blocks), dim3(kBlock), di.lds_pad,
-                           stream, arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
-    else if (variant == 32)  // plain (write-back) frame stores, sessions 1-2
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, false>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
-                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
-#endif
-    else  // write-through (sc1) frame stores: +1.2% on C1 push/pop over plain stores
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3(blocks), dim3(kBlock), di.lds_pad, stream,
-                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD); batches of 2 slots
+    // (94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, capping the occupancy lower
+    // slower still (profiles/r01_s2_occupancy.md). Frame stores write-through (sc1): +1.2% on C1
+    // push/pop over plain stores; dispatch order (the XCD-aware order measured 2% slower here).
+    hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3(blocks), dim3(kBlock), 0, stream, arena,
+                       arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     return hipGetLastError();
 }
 
@@ -1519,7 +1324,7 @@ DEV uint32_t be32x(uint32_t le) { return __builtin_bswap32(le); }
 
 // One packet per 8-lane row: c0 = frame bytes 16rl..16rl+15 (zeros past len; len 0 when the
 // descriptor is out of bounds, which yields the all-zero record and hash of a dead packet).
-template <int ST = 0>  // record stores: 0 plain, 1 nt, 2 write-through (sc1), measurement
+// record stores non-temporal (C1 +2% over plain; write-through measured no better)
 DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uint32_t rl,
                       uint32_t rowbase4, nfcs_flow_key* __restrict__ keys,
                       uint32_t* __restrict__ hashes) {
@@ -1584,15 +1389,13 @@ DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uin
         }
         if (p < n) {
             uint4* q = (uint4*)(keys + p) + rl;
-            if (ST == 1) __builtin_nontemporal_store(u32x4_t{r.x, r.y, r.z, r.w}, (u32x4_t*)q);
-            else if (ST == 2) st16<true>(q, r);
-            else *q = r;
+            __builtin_nontemporal_store(u32x4_t{r.x, r.y, r.z, r.w}, (u32x4_t*)q);
         }
     }
     if (hashes && rl == 0 && p < n) hashes[p] = hv;
 }
 
-template <int K, int ST = 1, int LD = 0, int BS = kBlock, bool XR = false>
+template <int K, int BS = kBlock>
 __global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            const nfcs_desc* __restrict__ desc,
@@ -1603,7 +1406,7 @@ __global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict
     constexpr uint32_t PR = 64 / R, PW = PR * K;  // rows per wave, packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = ((uint64_t)(XR ? xcd_block() : blockIdx.x) * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
+    const uint64_t pw = ((uint64_t)xcd_block() * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
     if (pw >= n) return;
     uint2 dl = make_uint2(0u, 0u);  // lane l: descriptor of packet pw + l
     if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
@@ -1618,52 +1421,22 @@ __global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict
         const bool live = pw + sl < n && off + (((uint64_t)dlen + 15u) & ~15ull) <= arena_bytes;
         L[k] = live ? dlen : 0u;
         const uint4* src = (const uint4*)(arena + (live ? off : 0));
-        c[k] = ld16<LD>((rl * 16u < L[k]) ? src + rl : &g_zero16);
+        c[k] = ld16<0>((rl * 16u < L[k]) ? src + rl : &g_zero16);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        flow_key_row<ST>(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
+        flow_key_row(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
 }
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,
-                            uint32_t* hashes, hipStream_t stream, int variant) {
+                            uint32_t* hashes, hipStream_t stream) {
     (void)di;
     if (n == 0) return hipSuccess;
-#define NFCS_FK(K, ST, LD)                                                                        \
-    hipLaunchKernelGGL((flow_keys_kernel<K, ST, LD>), dim3((n + 32u * K - 1u) / (32u * K)), dim3(kBlock), \
-                       0, stream, arena, arena_bytes, desc, n, keys, hashes)
-    switch (variant) {
-#ifdef NFCS_EXPERIMENTS
-    case 81: NFCS_FK(1, 0, 0); break;  // session 2: one slot, 8 packets per wave, plain stores
-    case 82: NFCS_FK(2, 0, 0); break;
-    case 88: NFCS_FK(8, 0, 0); break;
-    case 84: NFCS_FK(4, 0, 0); break;  // plain record stores (nt: C1 +1.5-2%)
-    case 85: NFCS_FK(4, 2, 0); break;  // write-through record stores
-    case 86: NFCS_FK(4, 1, 1); break;  // ... and non-temporal header loads
-#define NFCS_FKB(K, BS)                                                                           \
-    hipLaunchKernelGGL((flow_keys_kernel<K, 1, 0, BS>), dim3((n + (BS / 8) * K - 1u) / ((BS / 8) * K)), \
-                       dim3(BS), 0, stream, arena, arena_bytes, desc, n, keys, hashes)
-    case 90: NFCS_FKB(4, 64); break;   // one-wave workgroups
-    case 91: NFCS_FKB(4, 128); break;
-    case 92: NFCS_FKB(4, 512); break;
-    case 93: NFCS_FKB(2, 64); break;
-    case 94: NFCS_FKB(8, 64); break;
-    case 95: NFCS_FKB(1, 64); break;
-    case 96: NFCS_FKB(2, 128); break;
-    case 97: NFCS_FKB(3, 64); break;
-    case 98: NFCS_FKB(2, 256); break;
-    case 99: hipLaunchKernelGGL((flow_keys_kernel<4, 1, 0, kBlock, false>), dim3((n + 127u) / 128u),
-                                dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
-        break;  // dispatch order (no XCD remap)
-#undef NFCS_FKB
-#endif
-    default:  // 32 packets per wave, non-temporal record stores, XCD-aware block order (+1.5-2%)
-        hipLaunchKernelGGL((flow_keys_kernel<4, 1, 0, kBlock, true>), dim3((n + 127u) / 128u),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
-        break;
-    }
-#undef NFCS_FK
+    // 32 packets per wave (K = 4 slots of 8: K = 1 / 2 / 8 measured 0.59 / 0.68 / 0.67 against
+    // 0.72), non-temporal record stores (+1.5-2% over plain), XCD-aware block order (+1.5-2%)
+    hipLaunchKernelGGL((flow_keys_kernel<4>), dim3((n + 127u) / 128u),
+                       dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
     return hipGetLastError();
 }
 

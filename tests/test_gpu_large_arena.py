@@ -1,9 +1,15 @@
-"""The write-back store form of the checksum kernel (variant 30), which `nfcs_update_device`
-chooses for arenas of at least 2 GiB (kWriteBackArenaBytes), against the oracle
-and the reference: (a) forced on a fresh fuzz batch, byte for byte, status and patch records;
-(b) chosen by size on BASELINE C4 shards (4M x 1500 B = 6.3 GB), whose whole-arena digests must
-equal the reference's (tests/golden/configs.json, made from the compiled reference). Also split
-mode (variant 8) forced on fuzz frames."""
+"""The checksum kernel's store forms against the oracle and the reference.
+
+`nfcs_update_device` decides per wave of four packets, from their descriptor lengths alone: frames
+averaging at least kDeferMeanBytes (1280) write 8-byte patch records and a second, write-only pass
+stores them non-temporally; shorter frames store their bytes inline from the read pass. Covered:
+(a) fuzz frames in arena order (a mix of both forms) and sorted by length (long runs that all defer,
+short runs that all store inline), byte for byte with statuses and patch records, over two calls;
+(b) the same burst placed at the start of a > 2 GiB arena gives the same bytes as in an exact-size
+arena (the arena size never changes the result or the form); (c) BASELINE C4 shards (4M x 1500 B =
+6.3 GB, every wave deferred) against the reference's digests; (d) two streams sharing one context's
+deferred-store workspace; (e) zero-copy over a > 2 GiB pinned host arena (inline stores over PCIe).
+"""
 import json
 import os
 
@@ -15,48 +21,89 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEFER_MEAN = 1280  # kDeferMeanBytes (netflow_amd/csrc/nfcs_internal.h)
 
 
-@pytest.fixture
-def wb_engine(monkeypatch):
-    monkeypatch.setenv("NFCS_VARIANT", "30")  # read by nfcs_ctx_create
-    e = nf.Engine(0)
-    yield e
-    e.close()
+def deferred_waves(desc):
+    """Which groups of 4 packets the kernel defers (its rule, restated for the test)."""
+    lens = np.minimum(desc["len"].astype(np.int64), 0xFFFF)
+    pad = (-len(lens)) % 4
+    g = np.concatenate([lens, np.zeros(pad, np.int64)]).reshape(-1, 4).sum(axis=1)
+    return g >= 4 * DEFER_MEAN
 
 
-def test_write_back_form_fuzz_vs_oracle(wb_engine):
+def apply_patches(arena, desc, pt):
+    re = arena.copy()
+    for i in range(len(desc)):
+        o = int(desc[i]["off16"]) * 16
+        for f in ("ip", "l4"):
+            if pt[i][f + "_off"] != 0xFFFF:
+                re[o + int(pt[i][f + "_off"]): o + int(pt[i][f + "_off"]) + 2] = pt[i][f]
+    return re
+
+
+@pytest.mark.parametrize("order", ["arena", "by_length"])
+def test_store_forms_fuzz_vs_oracle(engine, order):
     frames = oracle.fuzz_frames(30, 0, 60000)
+    if order == "by_length":
+        frames = sorted(frames, key=len)
     for align in (16, 128):
         arena, desc = oracle.pack_frames(frames, align=align)
+        dw = deferred_waves(desc)
+        assert dw.any() and not dw.all()  # both forms in the same launch
+        n = len(desc)
+        d_arena = engine.alloc(arena.nbytes).upload(arena)
+        d_desc = engine.alloc(desc.nbytes).upload(desc)
+        d_st = engine.alloc(n)
+        d_pt = engine.alloc(8 * n)
+        ref = arena.copy()
+        for call in range(2):  # the second call runs over the updated frames (IHL < 5 overlaps
+            #                    change status on a second pass, in the reference as well)
+            rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+            before = d_arena.download(np.uint8, arena.nbytes)
+            # with caller patch records on the first call, into the workspace on the second
+            engine.update_device(d_arena, arena.nbytes, d_desc, n, d_st, d_pt if call == 0 else None)
+            engine.sync()
+            assert np.array_equal(d_st.download(np.uint8, n), rst)
+            assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
+            if call == 0:  # the records reproduce the update on the original frames
+                assert np.array_equal(apply_patches(before, desc, d_pt.download(nf.PATCH_DTYPE, n)), ref)
+        for b in (d_arena, d_desc, d_st, d_pt):
+            b.free()
+
+
+def test_small_burst_in_large_arena_same_bytes(engine):
+    """A short-frame burst at the start of a > 2 GiB arena (the round-1 size rule would have changed
+    the store form) and the same burst in its own exact-size arena: identical bytes and statuses,
+    both equal to the oracle; likewise a long-frame burst."""
+    for frames in (oracle.fuzz_frames(31, 0, 20000), [f for f in oracle.fuzz_frames(32, 0, 40000) if len(f) >= 1200]):
+        arena, desc = oracle.pack_frames(frames, align=128)
+        n = len(desc)
         ref = arena.copy()
         rst, _ = oracle.update_batch(ref, desc, nthreads=8)
-        n = len(desc)
-        d_arena = wb_engine.alloc(arena.nbytes).upload(arena)
-        d_desc = wb_engine.alloc(desc.nbytes).upload(desc)
-        d_st = wb_engine.alloc(n)
-        d_pt = wb_engine.alloc(8 * n)
-        wb_engine.update_device(d_arena, arena.nbytes, d_desc, n, d_st, d_pt)
-        wb_engine.sync()
-        assert np.array_equal(d_st.download(np.uint8, n), rst)
-        assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
-        pt = d_pt.download(nf.PATCH_DTYPE, n)
-        re = arena.copy()  # the patch records reproduce the update on the original frames
-        for i in range(n):
-            o = int(desc[i]["off16"]) * 16
-            for f in ("ip", "l4"):
-                if pt[i][f + "_off"] != 0xFFFF:
-                    re[o + int(pt[i][f + "_off"]): o + int(pt[i][f + "_off"]) + 2] = pt[i][f]
-        assert np.array_equal(re, ref)
+        big = (2 << 30) + 4096
+        outs = []
+        for nbytes in (arena.nbytes, big):
+            d_arena = engine.alloc(nbytes).upload(arena)
+            d_desc = engine.alloc(desc.nbytes).upload(desc)
+            d_st = engine.alloc(n)
+            engine.update_device(d_arena, nbytes, d_desc, n, d_st)
+            engine.sync()
+            outs.append((d_arena.download(np.uint8, arena.nbytes), d_st.download(np.uint8, n)))
+            for b in (d_arena, d_desc, d_st):
+                b.free()
+        for got, st in outs:
+            assert np.array_equal(st, rst)
+            assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("rank", [0, 7])
+@pytest.mark.parametrize("rank", [0, 3, 7])
 def test_c4_shard_digest_large_arena(engine, rank):
     g = json.load(open(os.path.join(GOLD, "configs.json")))
     sh = g["c4_rank_shards"][rank]
     n = sh["n"]
-    d_arena, nbytes, d_desc, _ = engine.config_batch(1, g["seed"], sh["first"], n, 128)
-    assert nbytes >= 2 << 30  # the size that selects the write-back form
+    d_arena, nbytes, d_desc, hdesc = engine.config_batch(1, g["seed"], sh["first"], n, 128)
+    assert deferred_waves(hdesc).all()
     assert f"{engine.digest_device(d_arena, nbytes, d_desc, n, sh['first']):016x}" == sh["digest_in"]
     engine.update_device(d_arena, nbytes, d_desc, n)
     engine.sync()
@@ -69,43 +116,43 @@ def test_c4_shard_digest_large_arena(engine, rank):
     d_desc.free()
 
 
-def test_split_mode_fuzz_vs_oracle(monkeypatch):
-    """Split mode forced on fuzz frames (variant 8: the product's form for large frames, chosen
-    by size only for C2-like batches, so the fuzz corpus never reaches it on its own), byte for
-    byte against the oracle over two successive calls."""
-    monkeypatch.setenv("NFCS_VARIANT", "8")
-    e = nf.Engine(0)
-    try:
-        frames = oracle.fuzz_frames(8, 0, 60000)
-        for align in (16, 128):
-            arena, desc = oracle.pack_frames(frames, align=align)
-            n = len(desc)
-            d_arena = e.alloc(arena.nbytes).upload(arena)
-            d_desc = e.alloc(desc.nbytes).upload(desc)
-            d_st = e.alloc(n)
-            ref = arena.copy()
-            # the second call runs over the updated frames; the oracle follows the same sequence (frames with IHL < 5 overlaps
-            # change status on a second pass, in the reference as well)
-            for _ in range(2):
-                rst, _ = oracle.update_batch(ref, desc, nthreads=8)
-                e.update_device(d_arena, arena.nbytes, d_desc, n, d_st)
-                e.sync()
-                assert np.array_equal(d_st.download(np.uint8, n), rst)
-                assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
-    finally:
-        e.close()
+def test_two_streams_share_the_workspace(engine):
+    """Back-to-back calls on one context from two streams, no caller patch records: both use the
+    context's deferred-store workspace; the second stream waits for the first's write pass."""
+    import torch
+    g = json.load(open(os.path.join(GOLD, "configs.json")))
+    s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+    b1 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
+    b2 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
+    for _ in range(3):
+        engine.gen_config_device(1, g["seed"], 0, 1 << 20, b1[0], b1[1], b1[2])
+        engine.gen_config_device(1, g["seed"], 0, 1 << 20, b2[0], b2[1], b2[2])
+        engine.sync()
+        engine.update_device(b1[0], b1[1], b1[2], 1 << 20, stream=s1.cuda_stream)
+        engine.update_device(b2[0], b2[1], b2[2], 1 << 20, stream=s2.cuda_stream)
+        s1.synchronize()
+        s2.synchronize()
+        want = g["configs"]["1"]["digest_out"]
+        for b in (b1, b2):
+            assert f"{engine.digest_device(b[0], b[1], b[2], 1 << 20, 0):016x}" == want
+    for b in (b1, b2):
+        b[0].free()
+        b[2].free()
 
 
 def test_zero_copy_large_pinned_arena(engine):
     """nfcs_update_host zero-copy over a pinned host arena of more than 2 GiB (1.4M C1 frames,
-    128-byte aligned, 2.15 GB): the size rule picks the write-back form for a kernel whose frames
-    live in host memory; statuses and every byte against the oracle."""
+    128-byte aligned, 2.15 GB): the kernel reads the frames over PCIe and stores the checksum bytes
+    inline (write-through); statuses and every byte against the oracle."""
     n = 1_400_000
     src, desc = oracle.gen_config(1, 20250620, 0, n, 128)
-    assert src.nbytes >= 2 << 30 and src.nbytes // n < 2048  # write-back form, not split mode
+    assert src.nbytes >= 2 << 30
     pinned = engine.host_array(src.nbytes)
-    pinned[:] = src
-    rst, _ = oracle.update_batch(src, desc, nthreads=8)
-    st = engine.update_host(pinned, desc, mode="zero_copy")
-    assert np.array_equal(st, rst)
-    assert np.array_equal(pinned, src)
+    try:
+        pinned[:] = src
+        rst, _ = oracle.update_batch(src, desc, nthreads=8)
+        st = engine.update_host(pinned, desc, mode="zero_copy")
+        assert np.array_equal(st, rst)
+        assert np.array_equal(pinned, src)
+    finally:
+        engine.host_free(pinned)

@@ -214,9 +214,46 @@ def test_host_path_pinned(engine, mode):
     frames = oracle.fuzz_frames(12, 0, 30000)
     packed, desc = oracle.pack_frames(frames)
     arena = engine.host_array(packed.nbytes)
-    arena[:] = packed
-    ref = packed.copy()
+    try:
+        arena[:] = packed
+        ref = packed.copy()
+        rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+        st = engine.update_host(arena, desc, mode=mode)
+        assert np.array_equal(st, rst)
+        assert np.array_equal(arena, ref)
+    finally:
+        engine.host_free(arena)
+
+
+@pytest.mark.parametrize("mode", ["patch", "frames"])
+def test_host_path_out_of_arena_descriptors_multi_chunk(engine, mode):
+    """Descriptors reaching past a > 64 MiB arena (len 0xFFFFFFFF; a length past the end) become
+    NFCS_ST_BAD_DESC in the middle of a multi-chunk staged call — every other frame as the oracle,
+    no error return, nothing left in flight."""
+    arena, desc = oracle.gen_config(1, SEED, 0, 50000)
+    assert arena.nbytes > 64 << 20
+    desc = desc.copy()
+    desc[100]["len"] = 0xFFFFFFFF
+    desc[30000]["len"] = arena.nbytes
+    ref = arena.copy()
     rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    assert rst[100] == nf.ST_BAD_DESC and rst[30000] == nf.ST_BAD_DESC
     st = engine.update_host(arena, desc, mode=mode)
     assert np.array_equal(st, rst)
     assert np.array_equal(arena, ref)
+
+
+def test_host_path_frame_larger_than_a_slot_is_rejected_untouched(engine):
+    """A frame inside the arena but larger than a 64 MiB staging slot cannot be staged: the call
+    returns NFCS_EINVAL before anything is queued, and the arena is unchanged."""
+    arena, desc = oracle.gen_config(1, SEED, 0, 1000)
+    big = np.zeros((65 << 20) + 4096, np.uint8)
+    big[: arena.nbytes] = arena
+    desc = desc.copy()
+    desc[500]["len"] = 65 << 20
+    desc[500]["off16"] = 0  # keeps arena order only with the frames before it moved too
+    desc = desc[500:]
+    before = big.copy()
+    with pytest.raises(nf.NfcsError):
+        engine.update_host(big, desc)
+    assert np.array_equal(big, before)
