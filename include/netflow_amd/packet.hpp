@@ -10,7 +10,7 @@
 // which gathers the frames into a pinned, 16-byte-aligned arena, runs the gfx950 engine
 // through the C ABI (include/nfcs.h), copies back 8-byte patch records and writes the 2+2
 // checksum bytes into each PacketBuffer in place — bit-exact with the reference; and
-// Packet::push_vlan / pop_vlan (packet.hpp:655-720) with their batched form
+// the batched form of Packet::push_vlan / pop_vlan (packet.hpp:655-720)
 //   netflow_amd::vlan_batch(Packet* const*, const uint32_t* ops, size_t, bool* ok)
 // (nfcs_vlan_device: tag insert / strip / re-tag and the checksums in one pass); the switch's
 // transit-IPv4 forward (switch.hpp:247-294) for a burst
@@ -20,8 +20,12 @@
 //   netflow_amd::flow_keys_batch(Packet* const*, size_t, nfcs_flow_key*, uint32_t* hashes)
 // (nfcs_flow_keys_device: 64-byte FlowKey records in host order + hash_flow values).
 //
-// All checksum arithmetic happens on the GPU; there is no CPU fallback. Constructing the
-// engine without a gfx950 device throws std::runtime_error ("fail loudly").
+// The batch entry points are templates over the packet type: they take this header's Packet or
+// the reference's own netflow::Packet (include/netflow_amd/netflow_adapter.hpp), whose buffers
+// offer the same PacketBuffer members. Bursts run on the GPU only — there is no CPU fallback, and
+// constructing the engine without a gfx950 device throws std::runtime_error ("fail loudly"). The
+// single-packet members (Packet::update_checksums, push_vlan, pop_vlan) run on the host CPU like
+// the reference's (include/netflow_amd/cpu_update.hpp): void / bool, never throwing.
 // Header-only; link with -lnfcs (netflow_amd/libnfcs.so).
 #pragma once
 
@@ -32,12 +36,14 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "nfcs.h"
+#include "netflow_amd/cpu_update.hpp"
 
 namespace netflow_amd {
 
@@ -137,45 +143,66 @@ public:
                                      std::to_string(device) + ": " + nfcs_strerror(rc));
         ctx_ = c;
     }
+    // Non-throwing form: *rc receives nfcs_ctx_create's result; the engine is usable iff it is 0.
+    ChecksumEngine(int device, std::nothrow_t, int* rc) noexcept {
+        nfcs_ctx* c = nullptr;
+        const int r = nfcs_ctx_create(device, &c);
+        if (rc) *rc = r;
+        ctx_ = r == NFCS_OK ? c : nullptr;
+    }
     ~ChecksumEngine() {
+        if (!ctx_) return;
         release();
         nfcs_ctx_destroy(ctx_);
     }
     ChecksumEngine(const ChecksumEngine&) = delete;
     ChecksumEngine& operator=(const ChecksumEngine&) = delete;
 
-    // Process-wide engine on device 0 (created on first use).
+    // Process-wide engine on device 0 (created on first use); throws if there is none.
     static ChecksumEngine& instance() {
-        static ChecksumEngine e(0);
-        return e;
+        ChecksumEngine* e = try_instance();
+        if (!e) throw std::runtime_error("netflow_amd: no gfx950 engine on device 0");
+        return *e;
+    }
+    // The same engine, or nullptr when none could be created (*rc: the nfcs error code). The batch
+    // free functions use this and return the code instead of throwing.
+    static ChecksumEngine* try_instance(int* rc = nullptr) noexcept {
+        static int err = NFCS_OK;
+        static ChecksumEngine e(0, std::nothrow, &err);
+        if (rc) *rc = err;
+        return err == NFCS_OK ? &e : nullptr;
     }
 
     // Batched Packet::update_checksums(): frames updated in place in their PacketBuffers.
     // status (optional) receives one NFCS_ST_* byte per packet. Returns 0 or an NFCS_E* code.
-    inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr);
+    // Pkt: netflow_amd::Packet or netflow::Packet (anything whose get_buffer() has the
+    // PacketBuffer window members).
+    template <class Pkt>
+    int update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* status = nullptr);
 
     // Batched Packet::push_vlan(vid, prio) / pop_vlan() (packet.hpp:655-720), each with the
     // update_checksums() it ends with. ops[i] is an NFCS_VLAN_* edit word (NFCS_VLAN_PUSH_OP(vid,
     // prio), NFCS_VLAN_POP or NFCS_VLAN_NOP); ok[i] (optional) receives what the reference call
     // returns; each PacketBuffer's data length changes as the reference changes it. The buffer's
     // room for a push is its capacity minus headroom (tailroom = that minus the length).
-    inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
-                          uint8_t* status = nullptr);
+    template <class Pkt>
+    int vlan_batch(Pkt* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
+                   uint8_t* status = nullptr);
 
     // Batched data path of the switch's transit-IPv4 forward (switch.hpp:247-294): for packet i
     // with an IPv4 header, TTL <= 1 -> NFCS_ST_TTL_EXPIRED and next_hop[i] >= table_n ->
     // NFCS_ST_NO_ROUTE (frame untouched, as the switch drops or punts it); otherwise TTL--,
     // dst/src MAC = table[next_hop[i]] and update_checksums(), status | NFCS_ST_FLAG_FWD. The
     // route and ARP lookups stay with the caller (next_hop indexes; NFCS_NH_NONE = no route).
-    inline int l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
-                                const nfcs_nexthop* table, uint32_t table_n,
-                                uint8_t* status = nullptr);
+    template <class Pkt>
+    int l3_forward_batch(Pkt* const* pkts, const uint32_t* next_hop, size_t n,
+                         const nfcs_nexthop* table, uint32_t table_n, uint8_t* status = nullptr);
 
     // PacketClassifier::extract_flow_key(pkt) and hash_flow(key) (packet_classifier.cpp:12-108)
     // for a batch: keys[i] (optional) = the FlowKey fields in host order (nfcs_flow_key, with
     // the hash in .hash), hashes[i] (optional) = hash_flow(key).
-    inline int flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
-                               uint32_t* hashes = nullptr);
+    template <class Pkt>
+    int flow_keys_batch(Pkt* const* pkts, size_t n, nfcs_flow_key* keys, uint32_t* hashes = nullptr);
 
     nfcs_ctx* ctx() const { return ctx_; }
 
@@ -198,7 +225,8 @@ private:
     };
     // Gather each packet's first min(len, limit) bytes (limit 0: all) into 16-byte aligned
     // slots of the pinned arena; returns the arena bytes used.
-    size_t gather(Packet* const* pkts, size_t n, size_t limit);
+    template <class Pkt>
+    size_t gather(Pkt* const* pkts, size_t n, size_t limit);
 
     void release() {
         if (h_arena_) nfcs_host_free(ctx_, h_arena_);
@@ -265,43 +293,43 @@ public:
 
     PacketBuffer* get_buffer() const { return buffer_; }
 
-    // packet.hpp:655 / 694, through the engine as a batch of one (each ends with
-    // update_checksums(), like the reference). Return what the reference returns.
-    bool push_vlan(uint16_t vlan_id_val, uint8_t priority = 0) {
-        return vlan_edit(NFCS_VLAN_PUSH_OP(vlan_id_val, priority));
+    // packet.hpp:655 / 694 on one packet, on the host CPU (cpu_update.hpp), each ending with
+    // update_checksums() like the reference; returns what the reference returns, never throws.
+    // Bursts: vlan_batch (GPU).
+    bool push_vlan(uint16_t vlan_id_val, uint8_t priority = 0) noexcept {
+        if (!buffer_) return false;
+        size_t len = buffer_->get_data_length();
+        const size_t room = buffer_->get_capacity() - buffer_->get_headroom();
+        if (!cpu::push_vlan(buffer_->get_data_start_ptr(), &len, room, vlan_id_val, priority)) return false;
+        return buffer_->set_data_len(len);
     }
-    bool pop_vlan() { return vlan_edit(NFCS_VLAN_POP); }
+    bool pop_vlan() noexcept {
+        if (!buffer_) return false;
+        size_t len = buffer_->get_data_length();
+        if (!cpu::pop_vlan(buffer_->get_data_start_ptr(), &len)) return false;
+        return buffer_->set_data_len(len);
+    }
 
-    // packet.hpp:722. Single packets go through the same GPU engine as a batch of one (a
-    // latency-bound use; batch with update_checksums_batch). void, like the reference.
-    void update_checksums() {
-        if (!buffer_) return;
-        Packet* self = this;
-        const int rc = ChecksumEngine::instance().update_checksums_batch(&self, 1);
-        if (rc != NFCS_OK) throw std::runtime_error(std::string("update_checksums: ") + nfcs_strerror(rc));
+    // packet.hpp:722 on one packet, on the host CPU (cpu_update.hpp): void, never throws, like
+    // the reference. A single packet would only pay a PCIe round trip on the GPU; bursts go to
+    // update_checksums_batch (GPU).
+    void update_checksums() noexcept {
+        if (buffer_) cpu::update_checksums(buffer_->get_data_start_ptr(), buffer_->get_data_length());
     }
 
 private:
-    bool vlan_edit(uint32_t op) {
-        if (!buffer_) return false;
-        Packet* self = this;
-        bool ok = false;
-        const int rc = ChecksumEngine::instance().vlan_batch(&self, &op, 1, &ok);
-        if (rc != NFCS_OK) throw std::runtime_error(std::string("vlan edit: ") + nfcs_strerror(rc));
-        return ok;
-    }
-
     PacketBuffer* buffer_;
 };
 
-inline int ChecksumEngine::update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status) {
+template <class Pkt>
+int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* status) {
     if (n == 0) return NFCS_OK;
     if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::lock_guard<std::mutex> lock(mu_);
     // gather: each frame at a 16-byte aligned offset of one pinned arena
     size_t bytes = 0;
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         bytes += ((b ? b->get_data_length() : 0) + 15) & ~size_t(15);
     }
     if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
@@ -324,7 +352,7 @@ inline int ChecksumEngine::update_checksums_batch(Packet* const* pkts, size_t n,
     // writes it first; applying in that order also reproduces IHL < 5 overlaps exactly)
     const nfcs_patch* pt = static_cast<const nfcs_patch*>(h_patch_);
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         if (!b) continue;
         unsigned char* f = b->get_data_start_ptr();
         if (pt[i].ip_off != NFCS_PATCH_NONE) { f[pt[i].ip_off] = pt[i].ip[0]; f[pt[i].ip_off + 1] = pt[i].ip[1]; }
@@ -333,8 +361,9 @@ inline int ChecksumEngine::update_checksums_batch(Packet* const* pkts, size_t n,
     return NFCS_OK;
 }
 
-inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok,
-                                      uint8_t* status) {
+template <class Pkt>
+int ChecksumEngine::vlan_batch(Pkt* const* pkts, const uint32_t* ops, size_t n, bool* ok,
+                               uint8_t* status) {
     if (n == 0) return NFCS_OK;
     if (!pkts || !ops || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::lock_guard<std::mutex> lock(mu_);
@@ -342,7 +371,7 @@ inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, 
     auto slot = [](size_t len) { return (len + 4 + 15) & ~size_t(15); };
     size_t bytes = 0;
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         bytes += slot(b ? b->get_data_length() : 0);
     }
     if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
@@ -354,7 +383,7 @@ inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, 
     uint32_t* hcaps = hops + pkt_cap_;
     size_t off = 0;
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         const size_t len = b ? b->get_data_length() : 0;
         if (len) std::memcpy(arena + off, b->get_data_start_ptr(), len);
         // bytes past the frame: the buffer's own bytes where it has them (a re-tag of a runt
@@ -385,7 +414,7 @@ inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, 
     if ((rc = nfcs_memcpy_d2h(ctx_, st.data(), d_status_, n))) return rc;
     // scatter: the edited window back into each PacketBuffer and its new data length
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         const bool done = (st[i] & NFCS_ST_FLAG_VLAN) != 0;
         if (ok) ok[i] = done;
         if (status) status[i] = st[i];
@@ -400,12 +429,13 @@ inline int ChecksumEngine::vlan_batch(Packet* const* pkts, const uint32_t* ops, 
     return NFCS_OK;
 }
 
-inline size_t ChecksumEngine::gather(Packet* const* pkts, size_t n, size_t limit) {
+template <class Pkt>
+size_t ChecksumEngine::gather(Pkt* const* pkts, size_t n, size_t limit) {
     uint8_t* arena = static_cast<uint8_t*>(h_arena_);
     nfcs_desc* desc = static_cast<nfcs_desc*>(h_desc_);
     size_t off = 0;
     for (size_t i = 0; i < n; ++i) {  // layout first
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         size_t len = b ? b->get_data_length() : 0;
         if (limit && len > limit) len = limit;
         desc[i] = nfcs_desc{static_cast<uint32_t>(off >> 4), static_cast<uint32_t>(len)};
@@ -431,15 +461,15 @@ inline size_t ChecksumEngine::gather(Packet* const* pkts, size_t n, size_t limit
     return off;
 }
 
-inline int ChecksumEngine::l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
-                                            const nfcs_nexthop* table, uint32_t table_n,
-                                            uint8_t* status) {
+template <class Pkt>
+int ChecksumEngine::l3_forward_batch(Pkt* const* pkts, const uint32_t* next_hop, size_t n,
+                                     const nfcs_nexthop* table, uint32_t table_n, uint8_t* status) {
     if (n == 0) return NFCS_OK;
     if (!pkts || !next_hop || (table_n && !table) || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::lock_guard<std::mutex> lock(mu_);
     size_t bytes = 0;
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         bytes += ((b ? b->get_data_length() : 0) + 15) & ~size_t(15);
     }
     if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
@@ -469,7 +499,7 @@ inline int ChecksumEngine::l3_forward_batch(Packet* const* pkts, const uint32_t*
     // the L4 checksum at most at l2 18 + IHL 60 + 16)
     for (size_t i = 0; i < n; ++i) {
         if (status) status[i] = st[i];
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         if (!b || !(st[i] & NFCS_ST_FLAG_FWD)) continue;
         const size_t len = desc[i].len, w = len < 128 ? len : 128;
         std::memcpy(b->get_data_start_ptr(), arena + (size_t)desc[i].off16 * 16, w);
@@ -477,8 +507,8 @@ inline int ChecksumEngine::l3_forward_batch(Packet* const* pkts, const uint32_t*
     return NFCS_OK;
 }
 
-inline int ChecksumEngine::flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
-                                           uint32_t* hashes) {
+template <class Pkt>
+int ChecksumEngine::flow_keys_batch(Pkt* const* pkts, size_t n, nfcs_flow_key* keys, uint32_t* hashes) {
     if (n == 0) return NFCS_OK;
     if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::lock_guard<std::mutex> lock(mu_);
@@ -625,24 +655,40 @@ inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uin
     return NFCS_OK;
 }
 
-// Free-function form on the process-wide engine.
+// Free-function forms on the process-wide engine: they return NFCS_ENODEV (or the error
+// nfcs_ctx_create reported) instead of throwing when no gfx950 engine exists.
+namespace detail {
+template <class F>
+int on_default_engine(F&& f) noexcept {
+    int rc = NFCS_OK;
+    ChecksumEngine* e = ChecksumEngine::try_instance(&rc);
+    if (!e) return rc ? rc : NFCS_ENODEV;
+    try {
+        return f(*e);
+    } catch (...) {  // std::bad_alloc from the host-side gather: the reference's only escape too
+        return NFCS_ENOMEM;
+    }
+}
+}  // namespace detail
+
 inline int update_checksums_batch(Packet* const* pkts, size_t n, uint8_t* status = nullptr) {
-    return ChecksumEngine::instance().update_checksums_batch(pkts, n, status);
+    return detail::on_default_engine([&](ChecksumEngine& e) { return e.update_checksums_batch(pkts, n, status); });
 }
 inline int update_checksums_batch(const std::vector<Packet*>& pkts, uint8_t* status = nullptr) {
     return update_checksums_batch(pkts.data(), pkts.size(), status);
 }
 inline int vlan_batch(Packet* const* pkts, const uint32_t* ops, size_t n, bool* ok = nullptr,
                       uint8_t* status = nullptr) {
-    return ChecksumEngine::instance().vlan_batch(pkts, ops, n, ok, status);
+    return detail::on_default_engine([&](ChecksumEngine& e) { return e.vlan_batch(pkts, ops, n, ok, status); });
 }
 inline int l3_forward_batch(Packet* const* pkts, const uint32_t* next_hop, size_t n,
                             const nfcs_nexthop* table, uint32_t table_n, uint8_t* status = nullptr) {
-    return ChecksumEngine::instance().l3_forward_batch(pkts, next_hop, n, table, table_n, status);
+    return detail::on_default_engine(
+        [&](ChecksumEngine& e) { return e.l3_forward_batch(pkts, next_hop, n, table, table_n, status); });
 }
 inline int flow_keys_batch(Packet* const* pkts, size_t n, nfcs_flow_key* keys,
                            uint32_t* hashes = nullptr) {
-    return ChecksumEngine::instance().flow_keys_batch(pkts, n, keys, hashes);
+    return detail::on_default_engine([&](ChecksumEngine& e) { return e.flow_keys_batch(pkts, n, keys, hashes); });
 }
 
 }  // namespace netflow_amd

@@ -2,11 +2,11 @@
 // netflow::Packet (tests/packet_test.cpp style), reading frames as hex lines on stdin.
 //   cpu     : PacketBuffer / Packet semantics; engine construction must fail loudly w/o GPU
 //   batch   : update_checksums_batch over all frames; prints "<status> <hex>" per frame
-//   single  : Packet::update_checksums() per frame; prints "<hex>" per frame
+//   single  : Packet::update_checksums() per frame (host CPU); prints "<hex>" per frame
 //   vlan    : lines "<op> <room> <hex>"; vlan_batch over all frames in zero-filled buffers with
 //             `room` bytes from the data start; prints "<ok> <status> <new len> <hex of room
 //             bytes from the data start>" per frame
-//   vlan1   : same through Packet::push_vlan / pop_vlan one packet at a time
+//   vlan1   : same through Packet::push_vlan / pop_vlan one packet at a time (host CPU)
 #include <netflow_amd/packet.hpp>
 
 #include <algorithm>
@@ -48,6 +48,21 @@ static int cpu_checks() {
     bool threw = false;
     try { ChecksumEngine e(0); } catch (const std::runtime_error&) { threw = true; }
     std::printf("engine_without_gpu_throws=%d\n", threw ? 1 : 0);
+    {   // the batch free functions return a code instead (the reference's calls never throw)
+        PacketBuffer b(128, 32, 60);
+        std::memset(b.get_data_start_ptr(), 0, 60);
+        Packet p(&b);
+        std::vector<Packet*> v{&p};
+        std::printf("batch_rc=%d\n", update_checksums_batch(v));
+        uint32_t op = NFCS_VLAN_POP;
+        bool ok = true;
+        std::printf("vlan_batch_rc=%d\n", vlan_batch(v.data(), &op, 1, &ok));
+        // single-packet members: host CPU, no engine needed, no throw
+        bad += p.pop_vlan() != false;                       // untagged: the reference returns false
+        bad += !p.push_vlan(5, 1) || b.get_data_length() != 64;
+        bad += !p.pop_vlan() || b.get_data_length() != 60;
+        p.update_checksums();
+    }
     std::printf("api_failures=%d\n", bad);
     return bad;
 }

@@ -30,6 +30,7 @@ def test_cpp_api_semantics_cpu(exe):
     assert "api_failures=0" in r.stdout, r.stdout + r.stderr
     if not os.path.exists("/dev/kfd"):
         assert "engine_without_gpu_throws=1" in r.stdout  # no silent CPU fallback
+        assert "batch_rc=-4" in r.stdout and "vlan_batch_rc=-4" in r.stdout  # NFCS_ENODEV, no throw
 
 
 def _frames():
@@ -39,9 +40,9 @@ def _frames():
     return frames
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["batch", "single"])
+@pytest.mark.parametrize("mode", [pytest.param("batch", marks=pytest.mark.gpu), "single"])
 def test_cpp_update_matches_oracle(exe, mode):
+    """update_checksums_batch (GPU) and Packet::update_checksums() (one packet, host CPU)."""
     frames = _frames() if mode == "batch" else _frames()[:200]
     r = subprocess.run([exe, mode], input="\n".join(f.hex() for f in frames) + "\n",
                        capture_output=True, text=True, timeout=300)
@@ -59,11 +60,11 @@ def test_cpp_update_matches_oracle(exe, mode):
             assert int(st) == est
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["vlan", "vlan1"])
+@pytest.mark.parametrize("mode", [pytest.param("vlan", marks=pytest.mark.gpu), "vlan1"])
 def test_cpp_vlan_matches_reference_behaviour(exe, mode):
-    """netflow_amd::vlan_batch and Packet::push_vlan / pop_vlan against the oracle (pinned to
-    the reference by tests/golden/kat_vlan.json / vlan_ref.npz): new bytes, length and return."""
+    """netflow_amd::vlan_batch (GPU) and Packet::push_vlan / pop_vlan (one packet, host CPU)
+    against the oracle (pinned to the reference by tests/golden/kat_vlan.json / vlan_ref.npz): new
+    bytes, length and return."""
     import numpy as np
     from vlan_common import random_vlan_case
     frames, ops, caps = random_vlan_case(77, 3000 if mode == "vlan" else 150)

@@ -1,0 +1,97 @@
+"""The boundary over NetFlow++'s OWN types (include/netflow_amd/netflow_adapter.hpp): a burst of
+`netflow::Packet` objects over `netflow::PacketBuffer`s — the reference's classes, compiled from its
+headers into tests/cpp/_ref/netflow_adapter_test by tests/cpp/Makefile — goes through
+`netflow_amd::update_checksums_batch` / `vlan_batch` on the GPU, and the reference's own
+`Packet::update_checksums()` / `push_vlan()` / `pop_vlan()` in the same process are the checker.
+The single-packet members of netflow_amd::Packet run on the CPU (include/netflow_amd/cpu_update.hpp)
+and are checked against the reference the same way, without a GPU.
+
+The binary is built here (this container has /root/reference); on the GPU box, which does not,
+the prebuilt binary that travels with the tree is run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "netflow_adapter_test")
+REF_INCLUDE = "/root/reference/include"
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def exe():
+    if os.path.isdir(REF_INCLUDE):
+        import netflow_amd as nf
+        if not os.path.exists(nf.LIB_PATH):
+            nf.build()
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "ref"], check=True)
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} is missing: build it where the reference headers are "
+                    "(make -C tests/cpp ref, run by __graft_entry__.build())")
+    return EXE
+
+
+def frames():
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "kat.json")))
+    return [bytes.fromhex(kat[k]["in"]) for k in sorted(kat)] + oracle.fuzz_frames(4242, 0, 20000)
+
+
+def vlan_input(seed, n):
+    from vlan_common import random_vlan_case
+    fr, ops, caps = random_vlan_case(seed, n)
+    return "\n".join(f"{int(o)} {int(c)} {f.hex()}" for o, c, f in zip(ops, caps, fr)) + "\n"
+
+
+def run(exe, mode, inp):
+    r = subprocess.run([exe, mode], input=inp, capture_output=True, text=True, timeout=600)
+    head = r.stdout.split("\n", 1)[0]
+    kv = dict(x.split("=") for x in head.split())
+    return r, {k: int(v) for k, v in kv.items()}
+
+
+def test_single_packet_cpu_path_matches_reference(exe):
+    """netflow_amd::Packet::update_checksums() (host CPU, void, no throw) against the reference's
+    Packet::update_checksums() on the same bytes; the batch free function without a GPU returns
+    NFCS_ENODEV instead of throwing."""
+    fr = frames()
+    r, kv = run(exe, "cpu", "\n".join(f.hex() for f in fr) + "\n")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv["frames"] == len(fr) and kv["mismatches"] == 0
+    assert kv["skipped"] < 100  # only frames whose IHL reaches past the end (reference UB)
+    if not os.path.exists("/dev/kfd"):
+        assert kv["adapter_rc"] == -4  # NFCS_ENODEV, not an exception
+
+
+def test_single_packet_vlan_cpu_path_matches_reference(exe):
+    """netflow_amd::Packet::push_vlan / pop_vlan (host CPU) against the reference's: return value,
+    data length and every buffer byte."""
+    r, kv = run(exe, "vcpu", vlan_input(77, 20000))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv["frames"] == 20000 and kv["mismatches"] == 0
+
+
+@pytest.mark.gpu
+def test_netflow_packet_burst_matches_reference(exe):
+    """std::vector<netflow::Packet*> through netflow_amd::update_checksums_batch on the GPU: every
+    frame equal to the reference's own per-packet update_checksums(), statuses equal to the
+    oracle's."""
+    fr = frames()
+    r, kv = run(exe, "gpu", "\n".join(f.hex() for f in fr) + "\n")
+    assert r.returncode == 0, r.stdout[:2000] + r.stderr
+    assert kv["frames"] == len(fr) and kv["mismatches"] == 0 and kv["rc"] == 0
+    st = [int(x) for x in r.stdout.strip().split("\n")[1:]]
+    assert st == [oracle.update_frame(f)[1] for f in fr]
+
+
+@pytest.mark.gpu
+def test_netflow_packet_vlan_burst_matches_reference(exe):
+    """netflow_amd::vlan_batch over netflow::Packet against the reference's push_vlan / pop_vlan:
+    return values, data lengths, every buffer byte."""
+    r, kv = run(exe, "vgpu", vlan_input(78, 20000))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv["frames"] == 20000 and kv["mismatches"] == 0 and kv["rc"] == 0
