@@ -2,31 +2,37 @@
 """bench.py — device-resident batched checksum throughput (BASELINE.json metric).
 
 A "step" is one pass of the hot path — NetFlow++'s Packet::update_checksums()
-(packet.hpp:722-890), batched on the gfx950 engine — over one batch of synthetic frames that
-is already resident in HBM. At N=1 the workload is BASELINE config C1 (1 M x 1500 B IPv4+UDP
-on 1 MI355X); with --gpus N > 1 it is BASELINE config C4 (32 M x 1500 B sharded across 8 GPUs):
-each rank owns its own batch of 4 M packets (packets [rank*n, (rank+1)*n)), so per-GPU work is
-fixed (weak scaling) and there is no collective on the data path: ranks only meet at the
-timing barriers.
+(packet.hpp:722-890), batched on the gfx950 engine (one nfcs_update_device call: the read pass and,
+for waves of long frames, the non-temporal write pass) — over one batch of synthetic frames that is
+already resident in HBM.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1] [--packets n] [--no-cpu]
-                  [--op update|l3fwd|flowkey]
+                  [--op update|l3fwd|flowkey|vlan] [--strong]
 
---op l3fwd measures the fused transit-IPv4 forward instead (TTL--, MAC rewrite,
-update_checksums; nfcs_l3_forward_device) on C1 with next hop i % 9 (8 = no route).
---op flowkey measures PacketClassifier::extract_flow_key + hash_flow (SURVEY.md §8 f4;
-nfcs_flow_keys_device: 64-byte records + u32 hashes) in packets/s.
+Workloads (BASELINE.json configs):
+  N = 1   config C1: 1M x 1500 B IPv4+UDP (configs[1]); the line also carries a `fresh` sub-line —
+          the same work rotated over 4 separately generated batches, so no launch re-processes
+          what the previous one just wrote (a NIC ring's steady state).
+  N > 1   config C4: 32M x 1500 B sharded as independent 4M-packet batches, one per GPU (also at 2
+          and 4 GPUs): per-GPU work fixed, scaling "weak". `--strong` instead splits ONE batch of
+          the config's size across the ranks by bytes (nfcs_shard_bytes; e.g. the mixed C3), whose
+          per-rank digests must sum to the reference's digest of the whole batch.
+Without a launcher, `--gpus N > 1` starts `torch.distributed.run` with N ranks as a child process
+(this process touches no GPU) and exits with its status; under a launcher WORLD_SIZE must equal N.
 
-Prints ONE JSON line on rank 0. `value` = sum over ranks of frame bytes per step / the max
-over ranks of the timed wall time per step. `roofline` uses the kernel's HIP-event time on its
-own stream; `cpu_baseline` times the reference update_checksums() (oracle/_ref, compiled from
-/root/reference) or, if that .so is absent, the oracle port, on a bounded sample on rank 0.
+Prints ONE JSON line on rank 0. `value` = sum over ranks of frame bytes per step / the max over
+ranks of the timed wall time per step. `roofline` uses the kernels' HIP-event time on the launch
+stream (one call = both passes); `cpu_baseline` times the reference update_checksums()
+(oracle/_ref, compiled from /root/reference) or, if that .so is absent, the oracle port, on a
+bounded sample on rank 0 at N = 1, on all allotted host cores and on one core.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,26 +41,23 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import netflow_amd as nf  # noqa: E402
+import netflow_amd as nf  # noqa: E402  (loads no library and touches no GPU until used)
 
 SEED = 20250620
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip parameters)
 # measured on the MI355X box (tools/stream_read.hip, tools/stream_rw.hip; profiles/r01_stream_microbench.md):
 STREAM_READ_GBPS = 7007.0  # best read-only stream (nt loads)
-STREAM_RW_GBPS = 4839.0    # best read stream with one in-place store per 1536-byte frame
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 C4_PACKETS_PER_GPU = 1 << 22
-# bench.py --packets 4194304 on one MI355X, session 4: 5218.8 / 5399.6 / 5424.6 GB/s on three
-# boxes (profiles/r01_s4_bench_c4_shard_1gpu*.json); the median
-C4_SHARD_1GPU_GBPS = 5399.6
-WORKLOAD = {
-    0: "C0: 1024 x 64 B IPv4 (header checksum only)",
-    1: "C1: 1M x 1500 B IPv4+UDP, device-resident",
-    2: "C2: 1M x 9000 B IPv4+TCP jumbo, device-resident",
-    3: "C3: 4M x U{64..1500} B IPv4 TCP/UDP mix, device-resident",
-}
-WORKLOAD_C4 = ("C4: 1500 B IPv4+UDP sharded as independent per-GPU batches, 4M packets per GPU "
-               "(32M over 8 GPUs), device-resident")
+FRESH_BATCHES = 4
+NAMES = {0: "C0: {n} x 64 B IPv4 (header checksum only)",
+         1: "C1: {n} x 1500 B IPv4+UDP, device-resident",
+         2: "C2: {n} x 9000 B IPv4+TCP jumbo, device-resident",
+         3: "C3: {n} x U{{64..1500}} B IPv4 TCP/UDP mix, device-resident"}
+
+
+def human(n: int) -> str:
+    return f"{n >> 20}M" if n % (1 << 20) == 0 else str(n)
 
 
 def dist_env():
@@ -65,12 +68,12 @@ def dist_env():
 
 
 class Dist:
-    """Barrier + max-over-ranks. Uses torch.distributed (RCCL via backend 'nccl' when GPUs
-    are visible to torch, else gloo); a no-op at world size 1."""
+    """Barrier + max/sum over ranks. torch.distributed (RCCL via backend 'nccl' when GPUs are
+    visible to torch, else gloo); a no-op at world size 1. Only the timing barriers and these
+    reductions cross ranks: the data path has no collective."""
 
     def __init__(self, ws, rank, local):
         self.ws, self.rank, self.local = ws, rank, local
-        self.pg = None
         if ws > 1:
             import torch
             import torch.distributed as dist
@@ -80,8 +83,8 @@ class Dist:
             dist.init_process_group(backend=backend)
             self.dist, self.torch, self.backend = dist, torch, backend
 
-    def _t(self, v):
-        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+    def _t(self, v, dtype=None):
+        t = self.torch.tensor([v], dtype=dtype or self.torch.float64)
         return t.cuda() if self.backend == "nccl" else t
 
     def barrier(self):
@@ -91,16 +94,32 @@ class Dist:
     def max(self, v: float) -> float:
         if self.ws == 1:
             return float(v)
-        t = self._t(v)
+        t = self._t(float(v))
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum(self, v: float) -> float:
         if self.ws == 1:
             return float(v)
-        t = self._t(v)
+        t = self._t(float(v))
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+    def sum_u64(self, v: int) -> int:
+        """Exact sum mod 2^64 (int64 all-reduce wraps in two's complement)."""
+        if self.ws == 1:
+            return int(v) % (1 << 64)
+        s = int(v) % (1 << 64)
+        t = self._t(s - (1 << 64) if s >= (1 << 63) else s, self.torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return int(t.item()) % (1 << 64)
+
+    def gather(self, v: float) -> list:
+        if self.ws == 1:
+            return [float(v)]
+        out = [self._t(0.0) for _ in range(self.ws)]
+        self.dist.all_gather(out, self._t(float(v)))
+        return [float(x.item()) for x in out]
 
     def close(self):
         if self.ws > 1:
@@ -117,16 +136,29 @@ def device_sync():
 
 
 def shard(rank: int, n_per_rank: int) -> tuple[int, int]:
-    """Packet index range of a rank (weak scaling: every rank owns n_per_rank packets)."""
+    """Weak scaling: rank r owns packets [r*n, (r+1)*n) of the seeded stream (uniform lengths, so
+    the byte balance of nfcs_shard_bytes is the packet-count split)."""
     return rank * n_per_rank, n_per_rank
 
 
-def golden_digest(config: int, first: int, n: int):
+def shard_strong(config: int, total: int, rank: int, ws: int) -> tuple[int, int]:
+    """Strong scaling: ONE batch of `total` packets split into contiguous ranges by frame bytes
+    (nfcs_shard_bytes)."""
+    desc, _ = nf.layout_config(config, SEED, 0, total, 128)
+    b = nf.shard_bytes(desc, ws)
+    return int(b[rank]), int(b[rank + 1] - b[rank])
+
+
+def golden():
     try:
-        g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+        return json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
     except OSError:
-        return None
-    c = g["configs"].get(str(config))
+        return {}
+
+
+def golden_digest(config: int, first: int, n: int):
+    g = golden()
+    c = g.get("configs", {}).get(str(config))
     if c and c["first"] == first and c["n"] == n:
         return c["digest_out"]
     if config == 1:
@@ -136,21 +168,34 @@ def golden_digest(config: int, first: int, n: int):
     return None
 
 
-def golden_l3():
+def cpu_info() -> dict:
+    model = None
     try:
-        g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
     except OSError:
-        return None
-    return g.get("l3fwd_c1")
+        pass
+    try:
+        allotted = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allotted = os.cpu_count()
+    return {"cpu_model": model, "nproc": allotted, "machine_cpus": os.cpu_count()}
 
 
-def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str = "update"):
-    """Reference update_checksums() on host cores over a bounded sample of the workload."""
+def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str = "update",
+                 one_core_seconds: float = 5.0):
+    """The reference's own update_checksums() (oracle/_ref, compiled from /root/reference) on the
+    host cores over a bounded sample of the workload: `threads` std::threads over contiguous slices,
+    then the same on one thread."""
     try:
         import oracle
     except Exception as e:  # pragma: no cover
         return {"value": None, "error": repr(e)}
     kind = "reference" if oracle.ref_available() else "port"
+    info = cpu_info()
+    threads = max(1, min(threads, info["nproc"] or threads))
     # at least ~1.2 GB so the sample streams from DRAM like the GPU batch, not from a large L3
     n = {0: 1024, 1: 1 << 20, 2: 1 << 17, 3: 1 << 21}[config]
     arena, desc = oracle.gen_config(config, SEED, 0, n)
@@ -159,82 +204,76 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
     if op == "flowkey":
         recs = np.zeros((n, 64), dtype=np.uint8)
         hashes = np.zeros(n, dtype=np.uint32)
-        if kind == "reference":
-            R = oracle.ref()
-            run = lambda: R.nfref_flow_keys_batch(oracle._ptr(arena), desc.ctypes.data, n,
-                                                  oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p),
-                                                  threads)
-        else:
+
+    def runner(t):
+        if op == "flowkey":
+            if kind == "reference":
+                R = oracle.ref()
+                return lambda: R.nfref_flow_keys_batch(oracle._ptr(arena), desc.ctypes.data, n,
+                                                       oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p), t)
             L = oracle.lib()
-            run = lambda: L.nfo_flow_keys_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
-                                                oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p))
-            threads = 1
-    elif op == "vlan":
-        # push_vlan(100, 3) / pop_vlan() alternately (each pass leaves the batch ready for the
-        # next), 1536-byte buffers: the frames are laid out 128-byte aligned as on the GPU
-        arena, desc = oracle.gen_config(config, SEED, 0, n, 128)
-        ops = [np.full(n, oracle.vlan_op("push", 100, 3), np.uint32),
-               np.full(n, oracle.vlan_op("pop"), np.uint32)]
-        flip = [0]
-        if kind == "reference":
-            R = oracle.ref()
+            return lambda: L.nfo_flow_keys_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
+                                                 oracle._ptr(recs), oracle._ptr(hashes, oracle._u32p))
+        if op == "vlan":
+            ops = [np.full(n, oracle.vlan_op("push", 100, 3), np.uint32), np.full(n, oracle.vlan_op("pop"), np.uint32)]
+            flip = [0]
 
             def run():
-                R.nfref_vlan_batch(oracle._ptr(arena), desc.ctypes.data,
-                                   oracle._ptr(ops[flip[0]], oracle._u32p), n, 1536, threads)
+                if kind == "reference":
+                    oracle.ref().nfref_vlan_batch(oracle._ptr(varena), vdesc.ctypes.data,
+                                                  oracle._ptr(ops[flip[0]], oracle._u32p), n, 1536, t)
+                else:
+                    oracle.vlan_batch(varena, vdesc, ops[flip[0]], None, cap_all=1536)
                 flip[0] ^= 1
-        else:
-            def run():
-                oracle.vlan_batch(arena, desc, ops[flip[0]], None, cap_all=1536)
-                flip[0] ^= 1
-            threads = 1
-    elif op == "l3fwd":
-        g = golden_l3()
-        table = np.frombuffer(bytes.fromhex(g["table"]), dtype=np.uint8).copy()
-        nh = (np.arange(n) % 9).astype(np.uint32)
+            return run
+        if op == "l3fwd":
+            table = np.frombuffer(bytes.fromhex(golden()["l3fwd_c1"]["table"]), dtype=np.uint8).copy()
+            nh = (np.arange(n) % 9).astype(np.uint32)
+            if kind == "reference":
+                R = oracle.ref()
+                return lambda: R.nfref_l3_forward_batch(oracle._ptr(arena), desc.ctypes.data,
+                                                        oracle._ptr(nh, oracle._u32p), n, oracle._ptr(table), 8, t)
+            L = oracle.lib()
+            return lambda: L.nfo_l3_forward_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data,
+                                                  oracle._ptr(nh, oracle._u32p), n, oracle._ptr(table), 8, None)
         if kind == "reference":
             R = oracle.ref()
-            run = lambda: R.nfref_l3_forward_batch(oracle._ptr(arena), desc.ctypes.data,
-                                                   oracle._ptr(nh, oracle._u32p), n,
-                                                   oracle._ptr(table), 8, threads)
-        else:
-            L = oracle.lib()
-            run = lambda: L.nfo_l3_forward_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data,
-                                                 oracle._ptr(nh, oracle._u32p), n,
-                                                 oracle._ptr(table), 8, None)
-            threads = 1
-    elif kind == "reference":
-        R = oracle.ref()
-        run = lambda: R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, n, threads)
-    else:
+            return lambda: R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, n, t)
         L = oracle.lib()
-        run = lambda: L.nfo_update_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n,
-                                         None, None, threads)
-    # l3fwd mutates TTLs (each pass forwards once): restore the frames before every pass,
-    # outside the timed part
+        return lambda: L.nfo_update_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n, None, None, t)
+
+    if op == "vlan":  # 1536-byte buffers, frames 128-byte aligned as on the GPU
+        varena, vdesc = oracle.gen_config(config, SEED, 0, n, 128)
+    # l3fwd mutates TTLs (each pass forwards once): restore the frames before every pass, untimed
     pristine = arena.copy() if op == "l3fwd" else None
-    run()  # warm
-    reps, el = 0, 0.0
-    while el < min_seconds:
-        if pristine is not None:
-            np.copyto(arena, pristine)
-        t0 = time.perf_counter()
-        run()
-        el += time.perf_counter() - t0
-        reps += 1
-    gbs = nbytes * reps / el / 1e9
-    if op == "flowkey":
-        return {"value": round(n * reps / el / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
-                "kind": kind, "sample": f"{n} packets of config C{config} x {reps} passes, "
-                                        f"{threads} threads, g++ -O2, {el:.1f} s"}
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes, "
-                      f"{threads} threads, g++ -O2, {el:.1f} s"}
+
+    def timed(t, seconds):
+        run = runner(t)
+        run()  # warm
+        reps, el = 0, 0.0
+        while el < seconds:
+            if pristine is not None:
+                np.copyto(arena, pristine)
+            t0 = time.perf_counter()
+            run()
+            el += time.perf_counter() - t0
+            reps += 1
+        return reps, el
+
+    port = kind == "port" and op != "update"  # the oracle's other batch entries are single-threaded
+    t_all = 1 if port else threads
+    reps, el = timed(t_all, min_seconds)
+    reps1, el1 = timed(1, one_core_seconds)
+    unit, scale = ("Mpkt/s", n / 1e6) if op == "flowkey" else ("GB/s", nbytes / 1e9)
+    return {"value": round(scale * reps / el, 3), "unit": unit, "cores": t_all, "kind": kind,
+            "one_core": round(scale * reps1 / el1, 3), **info,
+            "sample": f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes on "
+                      f"{t_all} threads ({el:.1f} s) and x {reps1} on 1 thread ({el1:.1f} s), g++ -O2"}
 
 
 def load_traffic(config: int, n: int, op: str = "update"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
-    for the default batch size of the config; None otherwise."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), for
+    the default batch size of the config; None otherwise."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         t = json.load(open(p)).get(f"C{config}" + ("" if op == "update" else f"_{op}"))
@@ -245,31 +284,71 @@ def load_traffic(config: int, n: int, op: str = "update"):
     return t
 
 
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(n: int) -> int:
+    """--gpus N > 1 without a launcher: N ranks under torch.distributed.run, started as a child
+    process (this process has made no GPU call), on 127.0.0.1."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=1, choices=[0, 1, 2, 3])
-    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config size)")
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config size; "
+                                                           "with --strong: of the whole batch)")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: split one batch across the ranks by bytes instead of one batch per GPU")
     ap.add_argument("--align", type=int, default=128,
                     help="frame start alignment in the arena: 128 = one L2 line per frame start, as "
                          "NIC/DPDK buffer rings lay frames out (16 = densely packed)")
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch sub-line")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
-
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}: launch N ranks for --gpus N",
+              file=sys.stderr)
+        sys.exit(2)
+
     D = Dist(ws, rank, local)
-    n = args.packets or DEFAULT_PACKETS[args.config]
-    c4 = ws > 1 and args.config == 1 and not args.packets
-    if c4:  # BASELINE C4: 32M x 1500 B over 8 GPUs = 4M packets per GPU (also at 2 and 4 GPUs)
-        n = C4_PACKETS_PER_GPU
-    first, n = shard(rank, n)
+    if ws > 1 and args.strong:
+        total = args.packets or DEFAULT_PACKETS[args.config]
+        first, n = shard_strong(args.config, total, rank, ws)
+        workload = NAMES[args.config].format(n=human(total)) + f", one batch split by bytes over {ws} GPUs"
+        scaling = "strong"
+    else:
+        c4 = ws > 1 and args.config == 1 and not args.packets
+        first, n = shard(rank, C4_PACKETS_PER_GPU if c4 else (args.packets or DEFAULT_PACKETS[args.config]))
+        if c4:  # BASELINE C4: 32M x 1500 B over 8 GPUs = 4M packets per GPU (also at 2 and 4 GPUs)
+            workload = ("C4: 1500 B IPv4+UDP sharded as independent per-GPU batches, 4M packets per GPU "
+                        "(32M over 8 GPUs), device-resident")
+        else:
+            workload = NAMES[args.config].format(n=human(n)) + (f" per GPU x {ws}" if ws > 1 else "")
+            if args.packets and args.config == 1:
+                workload = workload.replace("C1: ", "C1-shaped: ")
+        scaling = "weak"
 
     # NFCS_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a 1-GPU box
     eng = nf.Engine(int(os.environ.get("NFCS_BENCH_DEVICE", local)))
@@ -277,11 +356,13 @@ def main():
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
     l3 = args.op == "l3fwd"
+    fk = args.op == "flowkey"
+    extra_roofline = {}
     if l3:
         # every launch decrements TTL (64 in the generator): K + 1 launches per fresh batch
         if args.steps > 60:
             raise SystemExit("--op l3fwd: --steps <= 60 (TTL 64 runs out after 63 forwards)")
-        g3 = golden_l3()
+        g3 = golden()["l3fwd_c1"]
         table = np.frombuffer(bytes.fromhex(g3["table"]), dtype=np.uint8).copy()
         d_tab = eng.alloc(table.nbytes).upload(table)
         d_nh = eng.alloc(4 * n).upload(((np.arange(first, first + n)) % 9).astype(np.uint32))
@@ -289,13 +370,16 @@ def main():
         step = lambda: eng.l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8)
         regen = lambda: (eng.gen_config_device(args.config, SEED, first, n, d_arena, nbytes, d_desc),
                          eng.sync())
-    elif args.op == "flowkey":
+    elif fk:
         d_keys = eng.alloc(64 * n)
         d_hash = eng.alloc(4 * n)
-        # moved per packet: the header line (min(len, 128) bytes) + 8 B descriptor read,
-        # 64 B record + 4 B hash written
+        # moved per packet: the frame's first 128-byte line (every field the key reads lies below
+        # byte 82, which spans two 64-byte sectors of that line) + 8 B descriptor read, 64 B
+        # record + 4 B hash written. `frac` is on these bytes; `frac_needed_bytes` on the 82
+        # header bytes the key needs + the same 76.
         hdr = float(np.minimum(hdesc["len"].astype(np.float64), 128.0).sum())
         algo_bytes = hdr + 76.0 * n
+        needed = float(np.minimum(hdesc["len"].astype(np.float64), 82.0).sum()) + 76.0 * n
         step = lambda: eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
         regen = lambda: None
     elif args.op == "vlan":
@@ -347,8 +431,10 @@ def main():
     wall = D.max(t1 - t0)
     ms_per_step = wall / args.steps * 1e3
     total_frame_bytes = D.sum(frame_bytes)
+    rank_gbps = D.gather(frame_bytes / ((t1 - t0) / args.steps) / 1e9)
 
     # kernel duration with HIP events on the launch stream (roofline), same launches
+    got = None
     if l3:
         regen()
         ev_ms = eng.time_l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8,
@@ -363,7 +449,7 @@ def main():
         ev_ms = eng.time_vlan_device(d_arena, nbytes, d_desc, n, VPUSH, nf.VLAN_POP, VCAP,
                                      2 * ((args.steps + 1) // 2)) / (2 * ((args.steps + 1) // 2))
         # parity: one push of the untagged batch vs the reference's digest, then one pop
-        gv = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json"))).get("vlan_c1", {})
+        gv = golden().get("vlan_c1", {})
         on_ref = first == 0 and n == gv.get("n")
         step()
         eng.sync()
@@ -373,11 +459,11 @@ def main():
         want = gv.get("digest_push_pop") if on_ref else golden_digest(1, first, n)
         if on_ref and got_push != gv["digest_push"]:
             want = "push digest " + gv["digest_push"] + " != " + got_push
-    elif args.op == "flowkey":
+    elif fk:
         ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
                                           args.steps) / args.steps
         # parity: digest of the 64-byte records (they hold the hashes too) vs the reference's
-        gk = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json"))).get("flowkey_c1", {})
+        gk = golden().get("flowkey_c1", {})
         want = None
         if first == 0 and n == gk.get("n") and args.align == gk.get("align"):
             eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
@@ -386,22 +472,37 @@ def main():
             rdesc["len"] = 64
             d_rdesc = eng.alloc(rdesc.nbytes).upload(rdesc)
             eng.sync()
-            got_fk = f"{eng.digest_device(d_keys, 64 * n, d_rdesc, n, 0):016x}"
+            got = f"{eng.digest_device(d_keys, 64 * n, d_rdesc, n, 0):016x}"
             want = gk["digest_records"]
             d_rdesc.free()
+        extra_roofline = {"frac_needed_bytes": round(needed / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "needed_bytes_per_packet": "min(len, 82) header + 8 descriptor + 64 record + 4 hash",
+                          "frac_is_on": "min(len, 128): the frame's first 128-byte line, the two 64-byte "
+                                        "sectors the 82 header bytes span"}
     else:
         ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
         # parity of what was measured: digest of the updated arena vs the reference's
         want = golden_digest(args.config, first, n)
     achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
-    got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
-    if args.op == "flowkey" and want is not None:
-        got = got_fk
+    if got is None:
+        got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
     parity_ok = None if want is None else (got == want)
-    parity_all = D.sum(0.0 if parity_ok is False else 1.0) == ws
+    parity = {"digest": got, "reference_digest": want, "match": parity_ok}
+    if scaling == "strong" and args.op == "update":
+        # the per-rank digests are order-independent sums: together they must equal the reference's
+        # digest of the whole batch
+        whole = D.sum_u64(int(got, 16))
+        want_whole = golden_digest(args.config, 0, args.packets or DEFAULT_PACKETS[args.config])
+        parity = {"digest_all_ranks": f"{whole:016x}", "reference_digest": want_whole,
+                  "match": None if want_whole is None else f"{whole:016x}" == want_whole}
+        parity_ok = parity["match"]
+    parity["all_ranks"] = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    traffic = load_traffic(args.config, n, args.op) if args.align == 128 else None
-    fk = args.op == "flowkey"
+    fresh = None
+    if ws == 1 and args.op == "update" and not args.no_fresh and args.config in (1, 2, 3):
+        fresh = fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc)
+
+    traffic = load_traffic(args.config, n, args.op) if (args.align == 128 and ws == 1) else None
     total_packets = D.sum(float(n))
     out = {
         "metric": ("flow keys + hash_flow per second, batched packets, MI355X" if fk else
@@ -416,11 +517,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u16 one's-complement (u8 frames, u32 word sums)",
         "data": "synthetic (seeded generator, DESIGN.md §6), generated in HBM",
-        "config": {"workload": (WORKLOAD_C4 if c4 else WORKLOAD[args.config])
+        "config": {"workload": workload
                    + (", fused L3 forward (next hop i % 9)" if l3 else "")
                    + (", flow keys (header line only)" if fk else "")
                    + (", push_vlan(100, 3) / pop_vlan() alternating, 1536-byte buffers"
@@ -433,9 +534,11 @@ def main():
                      "traffic_read_write": None if traffic is None else
                      [int(traffic["fetch_bytes"]), int(traffic["write_bytes"])],
                      "kernel_ms": round(ev_ms, 4),
-                     "algorithmic_bytes_per_launch": int(algo_bytes)},
-        "parity": {"digest": got, "reference_digest": want, "match": parity_ok, "all_ranks": parity_all},
+                     "algorithmic_bytes_per_launch": int(algo_bytes), **extra_roofline},
+        "parity": parity,
     }
+    if ws > 1:
+        out["per_gpu_GBps"] = [round(x, 1) for x in rank_gbps]  # each rank's own rate, this run
     if args.op == "update":
         # frame-only and checksummed-only (frame minus its 14-byte L2 header;
         # the synthetic frames are untagged) rates, and the fraction of the read-only stream
@@ -447,15 +550,9 @@ def main():
                         "algorithmic_GBps_kernel": round(achieved, 1)}
         out["stream_ceiling"] = {"read_only_GBps": STREAM_READ_GBPS,
                                  "frac_of_read_only": round(achieved / STREAM_READ_GBPS, 4),
-                                 "read_plus_one_store_per_frame_GBps": STREAM_RW_GBPS,
                                  "source": "profiles/r01_stream_microbench.md"}
-    if c4:
-        # the same 4M-packet shard on ONE GPU (profiles/r01_s4_bench_c4_shard_1gpu.json): the
-        # per-GPU rate this line scales, lower than the N = 1 (C1, 1M-packet) line because a
-        # 6.3 GB batch does not stay partly cached between launches
-        out["one_gpu_same_shard"] = {"value": C4_SHARD_1GPU_GBPS, "unit": "GB/s",
-                                     "linear_at_n": round(C4_SHARD_1GPU_GBPS * ws, 1),
-                                     "source": "profiles/r01_s4_bench_c4_shard_1gpu.json"}
+    if fresh is not None:
+        out["fresh"] = fresh
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
@@ -465,6 +562,34 @@ def main():
     d_arena.free()
     eng.close()
     D.close()
+
+
+def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc):
+    """The same work rotated over FRESH_BATCHES separately generated batches (the timed one plus
+    FRESH_BATCHES - 1 more), so no launch runs over what the previous launch just wrote, as in a
+    NIC ring's steady state; wall clock around the steps, digests of every batch afterwards."""
+    extra = [eng.config_batch(args.config, SEED, first, n, args.align) for _ in range(FRESH_BATCHES - 1)]
+    batches = [(d_arena, nbytes, d_desc)] + [(a, b, d) for a, b, d, _ in extra]
+    steps = max(args.steps, 2 * FRESH_BATCHES)
+    for k in range(2 * FRESH_BATCHES):  # warm
+        a, b, d = batches[k % FRESH_BATCHES]
+        eng.update_device(a, b, d, n)
+    eng.sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        a, b, d = batches[k % FRESH_BATCHES]
+        eng.update_device(a, b, d, n)
+    eng.sync()
+    dt = (time.perf_counter() - t0) / steps
+    want = golden_digest(args.config, first, n)
+    digests = [f"{eng.digest_device(a, b, d, n, first):016x}" for a, b, d in batches]
+    for a, _, d, _ in extra:
+        a.free()
+        d.free()
+    return {"batches": FRESH_BATCHES, "steps": steps, "value": round(frame_bytes / dt / 1e9, 2),
+            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4),
+            "frac": round(algo_bytes / dt / 1e9 / HBM_PEAK_GBS, 4), "timing": "wall clock",
+            "parity": None if want is None else all(g == want for g in digests)}
 
 
 if __name__ == "__main__":

@@ -238,6 +238,15 @@ NFCS_API int nfcs_flow_keys_device(nfcs_ctx* ctx, const uint8_t* d_arena, uint64
                                    const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
                                    uint32_t* d_hash, void* stream);
 
+/* ---- multi-GPU partition ----------------------------------------------- */
+
+/* Split a batch into `parts` contiguous packet ranges balanced by frame bytes: part p owns packets
+ * [bounds[p], bounds[p+1]) (bounds has parts + 1 entries, bounds[0] = 0, bounds[parts] = n), and
+ * its frame bytes (sum of len) differ from total / parts by less than one frame. Packets are
+ * independent (packet.hpp:722-890 reads only its own frame), so each part goes to its own GPU with
+ * its own context and no collective. Pure host code. */
+NFCS_API int nfcs_shard_bytes(const nfcs_desc* h_desc, uint32_t n, uint32_t parts, uint32_t* bounds);
+
 /* ---- synthetic batches and digests (bench / parity support; not on the hot path) ------ */
 
 /* Lay out n frames of a config (packet indices first_index .. first_index+n-1), frame starts

@@ -82,6 +82,7 @@ def _declare(L):
         "nfcs_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
         "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
+        "nfcs_shard_bytes": ([_vp, _u32, _u32, _vp], ctypes.c_int),
         "nfcs_gen_config_device": ([_vp, ctypes.c_int, _u64, _u64, _u32, _vp, _u64, _vp, _vp], ctypes.c_int),
         "nfcs_digest_device": ([_vp, _vp, _u64, _vp, _u32, _u64, ctypes.POINTER(_u64), _vp], ctypes.c_int),
         "nfcs_device_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -139,6 +140,16 @@ def layout_config(config: int, seed: int, first: int, n: int, align: int = 16):
     _check(lib().nfcs_layout_config(config, seed, first, n, align, desc.ctypes.data if n else None,
                                     ctypes.byref(nbytes)), "nfcs_layout_config")
     return desc, int(nbytes.value)
+
+
+def shard_bytes(desc: np.ndarray, parts: int) -> np.ndarray:
+    """nfcs_shard_bytes: parts + 1 packet bounds; part p = packets [b[p], b[p+1]), its frame bytes
+    within one frame of total / parts (multi-GPU partition)."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    bounds = np.zeros(parts + 1, dtype=np.uint32)
+    _check(lib().nfcs_shard_bytes(desc.ctypes.data if len(desc) else None, len(desc), parts,
+                                  bounds.ctypes.data), "nfcs_shard_bytes")
+    return bounds
 
 
 class DeviceBuffer:

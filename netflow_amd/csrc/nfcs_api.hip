@@ -444,6 +444,25 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     return NFCS_OK;
 }
 
+NFCS_API int nfcs_shard_bytes(const nfcs_desc* h_desc, uint32_t n, uint32_t parts, uint32_t* bounds) {
+    if (!bounds || parts == 0 || (n && !h_desc)) return NFCS_EINVAL;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += h_desc[i].len;
+    // bounds[p] = the first packet at which the running byte count reaches p * total / parts, so
+    // every boundary lies within one frame of its ideal position
+    uint32_t i = 0;
+    uint64_t run = 0;
+    bounds[0] = 0;
+    for (uint32_t p = 1; p < parts; ++p) {
+        const unsigned __int128 t = (unsigned __int128)total * p;
+        const uint64_t target = (uint64_t)(t / parts) + (t % parts != 0);
+        while (i < n && run < target) run += h_desc[i++].len;
+        bounds[p] = i;
+    }
+    bounds[parts] = n;
+    return NFCS_OK;
+}
+
 NFCS_API int nfcs_layout_config(int config, uint64_t seed, uint64_t first_index, uint32_t n,
                                 uint32_t align, nfcs_desc* h_desc, uint64_t* arena_bytes) {
     if (config < 0 || config > 3 || align < 16 || (align & 15u)) return NFCS_EINVAL;

@@ -1,4 +1,5 @@
-"""Multi-process path of bench.py on CPU: world_size 2 over gloo (127.0.0.1).
+"""Multi-process path of bench.py on CPU: world_size 2 over gloo (127.0.0.1); the --gpus / WORLD_SIZE
+contract; the byte-balanced split of one batch (nfcs_shard_bytes).
 
 The checksum path shards by packets with no data-path collective: each rank
 owns packets [rank*n, (rank+1)*n) of the same seeded stream, and ranks only meet at the timing
@@ -33,9 +34,10 @@ def _worker(rank, ws, port, q):
     total = D.sum(float(n))
     din, dout, hist = oracle.config_digest(1, bench.SEED, first, n, 1)
     dsum = D.sum(float(dout % (1 << 40)))  # exact in float64 for 2 ranks
+    dsum64 = D.sum_u64(dout)
     D.barrier()
     D.close()
-    q.put((rank, first, n, mx, total, dout, dsum))
+    q.put((rank, first, n, mx, total, dout, dsum, dsum64))
 
 
 @pytest.mark.parametrize("ws", [2])
@@ -60,3 +62,55 @@ def test_two_rank_gloo_harness(ws):
     _, whole, _ = oracle.config_digest(1, 20250620, 0, 4096 * ws, 2)
     assert (sum(r[5] for r in res) % (1 << 64)) == whole
     assert all(r[6] == float(sum(x[5] % (1 << 40) for x in res)) for r in res)
+    assert all(r[7] == whole for r in res)  # the exact u64 all-reduce
+
+
+def _strong_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws),
+                      RANK=str(rank), LOCAL_RANK=str(rank), NFCS_DIST_BACKEND="gloo")
+    import bench
+    import oracle
+    D = bench.Dist(*bench.dist_env())
+    first, n = bench.shard_strong(3, 1 << 22, rank, ws)  # the C3 batch, split by bytes
+    import netflow_amd as nf
+    desc, _ = nf.layout_config(3, bench.SEED, first, n, 128)
+    nbytes = int(desc["len"].astype("i8").sum())
+    _, dout, _ = oracle.config_digest(3, bench.SEED, first, n, 4)
+    whole = D.sum_u64(dout)
+    D.close()
+    q.put((rank, first, n, nbytes, whole))
+
+
+def test_two_rank_gloo_strong_split_of_c3_by_bytes():
+    """ONE mixed-length batch (C3: 4M frames of U{64..1500} B) split over 2 ranks
+    into contiguous ranges balanced by bytes; the ranks' byte counts are within one frame of each
+    other and their (reference-pinned oracle) digests sum to the reference's digest of C3."""
+    import json
+    import oracle
+    oracle.build(ref=False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == 0 and res[0][1] + res[0][2] == res[1][1] and res[1][1] + res[1][2] == 1 << 22
+    assert abs(res[0][3] - res[1][3]) <= 1500
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs.json")))
+    want = int(g["configs"]["3"]["digest_out"], 16)
+    assert res[0][4] == res[1][4] == want
+
+
+def test_gpus_flag_must_match_world_size():
+    """Under a launcher WORLD_SIZE must equal --gpus: a mismatch exits non-zero before any GPU use."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--no-cpu"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

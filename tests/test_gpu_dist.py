@@ -1,8 +1,10 @@
-"""bench.py's N-rank path on a GPU box: two ranks launched as the driver launches
-N > 1 (torch.distributed.run, 127.0.0.1), both on cuda:0 here (NFCS_BENCH_DEVICE=0; gloo for the
-timing barriers, since RCCL needs one GPU per rank). Each rank owns its own 4M-packet shard of
-BASELINE config C4 and checks its digest against the reference's per-rank C4 digests; rank 0's
-JSON line must report every rank bit-exact, n_gpus 2 and weak scaling."""
+"""bench.py's N-rank path on a GPU box, both ranks on cuda:0 here
+(NFCS_BENCH_DEVICE=0; gloo for the timing barriers, since RCCL needs one GPU per rank):
+(a) `bench.py --gpus 2` with no launcher starts its own two ranks (torch.distributed.run as a child
+process); each owns its own 4M-packet shard of BASELINE config C4 and checks its digest against the
+reference's per-rank C4 digests; rank 0's one JSON line reports n_gpus 2, weak scaling, every rank
+bit-exact; (b) as the driver launches N > 1 (torch.distributed.run, 127.0.0.1), `--strong` over C3:
+one mixed batch split by bytes, the per-rank digests summing to the reference's C3 digest."""
 import json
 import os
 import socket
@@ -26,9 +28,9 @@ def _free_port():
 
 def test_two_ranks_one_gpu_bench_line():
     env = dict(os.environ, NFCS_BENCH_DEVICE="0", NFCS_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu"]
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -38,3 +40,19 @@ def test_two_ranks_one_gpu_bench_line():
     assert d["config"]["packets_per_gpu"] == 1 << 22
     assert d["parity"]["match"] is True and d["parity"]["all_ranks"] is True
     assert d["value"] > 0 and d["roofline"]["kernel_ms"] > 0
+    assert len(d["per_gpu_GBps"]) == 2
+
+
+def test_two_ranks_strong_split_c3():
+    env = dict(os.environ, NFCS_BENCH_DEVICE="0", NFCS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "3", "--strong", "--steps", "3",
+           "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["parity"]["match"] is True and d["parity"]["all_ranks"] is True
