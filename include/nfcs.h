@@ -121,6 +121,11 @@ NFCS_API int nfcs_last_hip_error(void);
 NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out);
 NFCS_API int nfcs_ctx_destroy(nfcs_ctx* ctx);
 NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t */
+/* The host staging ring of nfcs_update_host (allocated by this call if not yet): *node = the GPU's
+ * NUMA node (-1 if unknown), *local = 1 when the ring's pinned memory is bound to that node (its
+ * copy threads then run on that node's CPUs). SURVEY.md §8e: one GPU per host thread, staging
+ * NUMA-local to each GPU. */
+NFCS_API int nfcs_ctx_host_numa(nfcs_ctx* ctx, int* node, int* local);
 
 /* ---- the hot path --------------------------------------------------------------------- */
 

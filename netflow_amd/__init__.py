@@ -83,6 +83,7 @@ def _declare(L):
         "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
         "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
         "nfcs_shard_bytes": ([_vp, _u32, _u32, _vp], ctypes.c_int),
+        "nfcs_ctx_host_numa": ([_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "nfcs_gen_config_device": ([_vp, ctypes.c_int, _u64, _u64, _u32, _vp, _u64, _vp, _vp], ctypes.c_int),
         "nfcs_digest_device": ([_vp, _vp, _u64, _vp, _u32, _u64, ctypes.POINTER(_u64), _vp], ctypes.c_int),
         "nfcs_device_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -216,6 +217,12 @@ class Engine:
     @property
     def stream(self) -> int:
         return lib().nfcs_ctx_stream(self.ctx)
+
+    def host_numa(self) -> tuple[int, bool]:
+        """(NUMA node of this GPU or -1, whether the host staging ring is bound to it)."""
+        node, local = ctypes.c_int(), ctypes.c_int()
+        _check(lib().nfcs_ctx_host_numa(self.ctx, ctypes.byref(node), ctypes.byref(local)), "host_numa")
+        return node.value, bool(local.value)
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)

@@ -5,8 +5,14 @@
 // Boundary being replaced: netflow::Packet::update_checksums() (packet.hpp:722-890), a void
 // member that never throws and silently skips malformed packets. Here every entry point returns
 // an int (0 or a negative NFCS_E*), never throws, and reports per-packet outcomes as status bytes.
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <new>
@@ -15,8 +21,22 @@
 
 #include "nfcs_internal.h"
 
+// Pinned host memory for the staging ring, on the GPU's NUMA node when that is known: mmap'd,
+// bound to the node (mbind, MPOL_PREFERRED), faulted in there, then registered with HIP; else
+// hipHostMalloc.
+struct HostBlock {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool mapped = false;  // mmap + hipHostRegister (free with hipHostUnregister + munmap)
+};
+
 struct nfcs_ctx {
     nfcs::DevInfo di;
+    int numa_node = -1;     // the GPU's NUMA node (sysfs), -1 if unknown
+    bool numa_local = false;  // staging memory bound to it
+    bool have_cpus = false;   // copy threads pinned to its CPUs
+    cpu_set_t node_cpus;
+    HostBlock hb[2];
     hipStream_t stream = nullptr;
     // host pipeline (nfcs_update_host)
     static constexpr int kSlots = 2;
@@ -90,9 +110,87 @@ int hip_fail(hipError_t e) {
 
 hipStream_t pick(nfcs_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
+// The GPU's NUMA node from sysfs (PCI bus id -> /sys/bus/pci/devices/<id>/numa_node), -1 if unknown.
+int gpu_numa_node(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char* q = bus; *q; ++q) *q = (char)((*q >= 'A' && *q <= 'F') ? *q - 'A' + 'a' : *q);
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE* f = fopen(path, "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    return node;
+}
+
+// The CPUs of a NUMA node (/sys/devices/system/node/node<N>/cpulist, e.g. "0-31,128-159").
+bool node_cpus(int node, cpu_set_t* set) {
+    char path[96];
+    snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+    FILE* f = fopen(path, "r");
+    if (!f) return false;
+    char buf[4096] = {0};
+    const bool ok = fgets(buf, sizeof(buf), f) != nullptr;
+    fclose(f);
+    if (!ok) return false;
+    CPU_ZERO(set);
+    int n = 0;
+    for (char* q = buf; *q && *q != '\n';) {
+        char* e;
+        const long a = strtol(q, &e, 10);
+        if (e == q) break;
+        long b = a;
+        if (*e == '-') b = strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n) CPU_SET((int)c, set);
+        q = (*e == ',') ? e + 1 : e;
+    }
+    return n > 0;
+}
+
+hipError_t host_block_alloc(HostBlock& b, size_t bytes, int node, bool* local) {
+    b.bytes = bytes;
+    *local = false;
+    if (node >= 0 && node < 1024) {
+        void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p != MAP_FAILED) {
+            unsigned long mask[16] = {0};
+            mask[node / 64] |= 1ul << (node % 64);
+            // MPOL_PREFERRED (1): the node's memory while it has free pages, never a failure
+            const bool bound = syscall(SYS_mbind, p, bytes, 1, mask, 16 * 64 + 1, 0) == 0;
+            memset(p, 0, bytes);  // fault the pages in on the node
+            if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) {
+                b.p = p;
+                b.mapped = true;
+                *local = bound;
+                return hipSuccess;
+            }
+            (void)hipGetLastError();
+            munmap(p, bytes);
+        }
+    }
+    return hipHostMalloc(&b.p, bytes, hipHostMallocDefault);
+}
+
+void host_block_free(HostBlock& b) {
+    if (!b.p) return;
+    if (b.mapped) {
+        (void)hipHostUnregister(b.p);
+        munmap(b.p, b.bytes);
+    } else {
+        (void)hipHostFree(b.p);
+    }
+    b = HostBlock{};
+}
+
 // memcpy split across threads: one host thread copies pageable memory at ~15-25 GB/s, below
-// what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned).
-void par_memcpy(void* dst, const void* src, size_t bytes, int threads) {
+// what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned). The helper
+// threads run on the GPU's NUMA node when its CPUs are known (cpus), next to the staging memory.
+void par_memcpy(void* dst, const void* src, size_t bytes, int threads, const cpu_set_t* cpus) {
     const size_t kMin = 4u << 20;
     if (threads <= 1 || bytes < 2 * kMin) {
         memcpy(dst, src, bytes);
@@ -104,7 +202,10 @@ void par_memcpy(void* dst, const void* src, size_t bytes, int threads) {
     for (size_t i = 1; i < t; ++i) {
         const size_t o = i * per;
         if (o >= bytes) break;
-        th.emplace_back([=] { memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o)); });
+        th.emplace_back([=] {
+            if (cpus) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), cpus);
+            memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
+        });
     }
     memcpy(dst, src, std::min(per, bytes));
     for (auto& x : th) x.join();
@@ -115,20 +216,32 @@ int ensure_host_pipeline(nfcs_ctx* ctx) {
     ctx->copy_threads = 8;
     ctx->stage_bytes = nfcs_ctx::kStageBytes;
     ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
+    // staging ring on the GPU's NUMA node, copy threads on its CPUs
+    ctx->numa_node = gpu_numa_node(ctx->di.device);
+    ctx->have_cpus = ctx->numa_node >= 0 && node_cpus(ctx->numa_node, &ctx->node_cpus);
+    const size_t a_desc = (size_t)ctx->stage_pkts * sizeof(nfcs_desc);
+    const size_t a_patch = (size_t)ctx->stage_pkts * sizeof(nfcs_patch);
+    const size_t a_status = ((size_t)ctx->stage_pkts + 4095) & ~size_t(4095);
+    bool local = true;
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         NFCS_HIP(hipStreamCreateWithFlags(&ctx->hs[s], hipStreamNonBlocking));
         NFCS_HIP(hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming));
         NFCS_HIP(hipMalloc(&ctx->d_arena[s], ctx->stage_bytes));
-        NFCS_HIP(hipMalloc(&ctx->d_desc[s], (size_t)ctx->stage_pkts * sizeof(nfcs_desc)));
+        NFCS_HIP(hipMalloc(&ctx->d_desc[s], a_desc));
         NFCS_HIP(hipMalloc(&ctx->d_status[s], ctx->stage_pkts));
-        NFCS_HIP(hipMalloc(&ctx->d_patch[s], (size_t)ctx->stage_pkts * sizeof(nfcs_patch)));
-        NFCS_HIP(hipHostMalloc(&ctx->h_arena[s], ctx->stage_bytes, hipHostMallocDefault));
-        NFCS_HIP(hipHostMalloc(&ctx->h_desc[s], (size_t)ctx->stage_pkts * sizeof(nfcs_desc),
-                               hipHostMallocDefault));
-        NFCS_HIP(hipHostMalloc(&ctx->h_status[s], ctx->stage_pkts, hipHostMallocDefault));
-        NFCS_HIP(hipHostMalloc(&ctx->h_patch[s], (size_t)ctx->stage_pkts * sizeof(nfcs_patch),
-                               hipHostMallocDefault));
+        NFCS_HIP(hipMalloc(&ctx->d_patch[s], a_patch));
+        // one pinned block per slot: arena | descriptors | patch records | statuses
+        bool l = false;
+        NFCS_HIP(host_block_alloc(ctx->hb[s], ctx->stage_bytes + a_desc + a_patch + a_status,
+                                  ctx->numa_node, &l));
+        local = local && l;
+        uint8_t* p = static_cast<uint8_t*>(ctx->hb[s].p);
+        ctx->h_arena[s] = p;
+        ctx->h_desc[s] = reinterpret_cast<nfcs_desc*>(p + ctx->stage_bytes);
+        ctx->h_patch[s] = reinterpret_cast<nfcs_patch*>(p + ctx->stage_bytes + a_desc);
+        ctx->h_status[s] = p + ctx->stage_bytes + a_desc + a_patch;
     }
+    ctx->numa_local = local;
     return NFCS_OK;
 }
 
@@ -263,10 +376,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
         (void)hipFree(c->d_desc[s]);
         (void)hipFree(c->d_status[s]);
         (void)hipFree(c->d_patch[s]);
-        if (c->h_arena[s]) (void)hipHostFree(c->h_arena[s]);
-        if (c->h_desc[s]) (void)hipHostFree(c->h_desc[s]);
-        if (c->h_status[s]) (void)hipHostFree(c->h_status[s]);
-        if (c->h_patch[s]) (void)hipHostFree(c->h_patch[s]);
+        host_block_free(c->hb[s]);
     }
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);
@@ -279,6 +389,15 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
 }
 
 NFCS_API void* nfcs_ctx_stream(nfcs_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+NFCS_API int nfcs_ctx_host_numa(nfcs_ctx* c, int* node, int* local) {
+    if (!c || !node || !local) return NFCS_EINVAL;
+    const int rc = ensure_host_pipeline(c);
+    if (rc) return rc;
+    *node = c->numa_node;
+    *local = c->numa_local ? 1 : 0;
+    return NFCS_OK;
+}
 
 NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
@@ -380,7 +499,8 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                 if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
             }
         } else if (!pinned) {
-            par_memcpy(h_arena + k.base, c->h_arena[s], k.bytes, c->copy_threads);
+            par_memcpy(h_arena + k.base, c->h_arena[s], k.bytes, c->copy_threads,
+                       c->have_cpus ? &c->node_cpus : nullptr);
         }
         if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
     };
@@ -405,7 +525,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint64_t bytes = end - base;
         const uint8_t* src = h_arena + base;
         if (!pinned) {
-            par_memcpy(c->h_arena[s], src, bytes, c->copy_threads);
+            par_memcpy(c->h_arena[s], src, bytes, c->copy_threads, c->have_cpus ? &c->node_cpus : nullptr);
             src = c->h_arena[s];
         }
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));

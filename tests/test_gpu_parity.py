@@ -225,6 +225,16 @@ def test_host_path_pinned(engine, mode):
         engine.host_free(arena)
 
 
+def test_host_staging_numa(engine):
+    """The staging ring of nfcs_update_host is placed on the GPU's NUMA node when sysfs names one
+    (SURVEY.md §8e); a node it reports exists on this host."""
+    node, local = engine.host_numa()
+    print(f"gpu numa node {node}, staging bound to it: {local}")
+    assert node >= -1
+    if node >= 0:
+        assert os.path.exists(f"/sys/devices/system/node/node{node}")
+
+
 @pytest.mark.parametrize("mode", ["patch", "frames"])
 def test_host_path_out_of_arena_descriptors_multi_chunk(engine, mode):
     """Descriptors reaching past a > 64 MiB arena (len 0xFFFFFFFF; a length past the end) become

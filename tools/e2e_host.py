@@ -41,6 +41,8 @@ def main(n=1 << 20, reps=5):
     want = int(json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
                ["configs"]["1"]["digest_out"], 16)
     pinned = eng.host_array(nbytes)
+    node, local = eng.host_numa()
+    print(json.dumps({"gpu_numa_node": node, "staging_bound_to_node": local}), flush=True)
     for mode in ("pageable_frames", "pageable_patch", "pinned_frames", "pinned_patch", "pinned_zero_copy"):
         arena = pinned if mode.startswith("pinned") else np.empty(nbytes, dtype=np.uint8)
         kw = dict(want_status=False, mode=mode.split("_", 1)[1])
@@ -56,9 +58,12 @@ def main(n=1 << 20, reps=5):
         assert result_digest(eng, arena, d_desc, n) == want, mode
         t = min(ts)
         r = {"mode": mode, "packets": n, "frame_bytes": frame_bytes, "seconds": t,
-             "GBps": frame_bytes / t / 1e9, "digest": f"{want:016x}"}
+             "GBps": frame_bytes / t / 1e9, "digest": f"{want:016x}", "numa_node": node,
+             "staging_numa_local": local}
         print(json.dumps(r), flush=True)
         out.append(r)
+    eng.host_free(pinned)
+    eng.close()
     return out
 
 

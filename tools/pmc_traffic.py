@@ -24,31 +24,35 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 
 
-KERNEL = {"update": "update_rows_kernel", "l3fwd": "update_rows_kernel", "vlan": "vlan_rows_kernel",
-          "flowkey": "flow_keys_kernel"}
+# the kernels of one call of the op: nfcs_update_device is the read pass and, for waves of long
+# frames, the write pass (apply_bytes_kernel); per call = the sum of the per-kernel medians
+KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("update_rows_kernel",),
+          "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_kernel",)}
 
 
 def run_pass(out, cfg, counters, steps, op="update"):
-    """One rocprofv3 pass with the given counters; median per counter over the op's launches."""
+    """One rocprofv3 pass with the given counters; per counter, the sum over the op's kernels of
+    the median over that kernel's launches."""
     d = os.path.join(out, f"c{cfg}_{op}_{counters[0]}")
     cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--op", op]
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--op", op]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 failed ({r.returncode}): {r.stderr[-2000:]}")
-    vals = {c: [] for c in counters}
+    vals = {(k, c): [] for k in KERNEL[op] for c in counters}
     for root, _, files in os.walk(d):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for row in csv.DictReader(open(os.path.join(root, f))):
-                    if KERNEL[op] in row["Kernel_Name"] and row["Counter_Name"] in vals:
-                        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    for c, v in vals.items():
-        if not v:
-            raise SystemExit(f"no {c} samples for {KERNEL[op]} in {d}")
-    return {c: statistics.median(v) for c, v in vals.items()}, min(len(v) for v in vals.values())
+                    for k in KERNEL[op]:
+                        if k in row["Kernel_Name"] and (k, row["Counter_Name"]) in vals:
+                            vals[(k, row["Counter_Name"])].append(float(row["Counter_Value"]))
+    if not vals[(KERNEL[op][0], counters[0])]:
+        raise SystemExit(f"no {counters[0]} samples for {KERNEL[op][0]} in {d}")
+    med = {c: sum(statistics.median(vals[(k, c)]) for k in KERNEL[op] if vals[(k, c)]) for c in counters}
+    return med, len(vals[(KERNEL[op][0], counters[0])])
 
 
 def main():
