@@ -11,6 +11,8 @@
 //   5 dense 8 B, sc1                       6 dense 8 B, nt
 //   7 4 KiB array, sc1                     8 dense, one 16-byte store per wave (4 packets)
 //   9 in place, 1 in 16 packets            10 dense 8 B, 1 in 16 packets
+//  11 the frame's first 64 bytes in place from lanes 0-3 (16 B each), plain
+//  12 the same, write-through (sc1)        13 the same, nt        14 the same, sc0 sc1 nt
 // Prints one JSON line per (packets, mode): average and best kernel time of 10 launches (HIP events).
 //   hipcc --offload-arch=gfx950 -O3 tools/wr_probe.hip -o tools/wr_probe && tools/wr_probe [M ...]
 #include <hip/hip_runtime.h>
@@ -71,6 +73,17 @@ __global__ __launch_bounds__(256) void probe(uint8_t* __restrict__ arena, uint32
             uint32_t* q = (uint32_t*)(f + 24);
             if (MODE == 4) __hip_atomic_store(q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else *q = acc;
+        }
+    } else if (MODE >= 11 && MODE <= 14) {
+        if (rl < 4) {  // the header slot's chunk rl, one byte changed: a full 64-byte segment
+            uint4 v0 = v[0];
+            v0.x ^= acc & 0xFFu;
+            const u32x4_t t = {v0.x, v0.y, v0.z, v0.w};
+            u32x4_t* q = (u32x4_t*)f + rl;
+            if (MODE == 12) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(q), "v"(t) : "memory");
+            else if (MODE == 13) __builtin_nontemporal_store(t, q);
+            else if (MODE == 14) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(q), "v"(t) : "memory");
+            else *q = t;
         }
     } else if (MODE == 8) {
         // the wave's four row sums in lane 0 as one 16-byte store
@@ -208,6 +221,10 @@ int main(int argc, char** argv) {
         run<8>(arena, n, dense, tiny);
         run<9>(arena, n, dense, tiny);
         run<10>(arena, n, dense, tiny);
+        run<11>(arena, n, dense, tiny);
+        run<12>(arena, n, dense, tiny);
+        run<13>(arena, n, dense, tiny);
+        run<14>(arena, n, dense, tiny);
         run<0>(arena, n, dense, tiny);
         (void)hipFree(arena);
         (void)hipFree(dense);
