@@ -11,10 +11,85 @@
 //           3   SF_DEFER in one-wave workgroups whatever the footprint
 //           4   SF_DEFER in 256-thread workgroups whatever the footprint
 //           5   the read pass only, records for every packet (SF_RECORDS) — no frame writes
+//           6   two row groups per wave, the second landing in LDS (8 packets per wave), 1-wave WGs
+//           7   the same in 256-thread workgroups
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
 namespace nfcs {
+
+// Two row groups per wave, the second landing in LDS (variants 6/7): group B's six chunk slots
+// are LDS-DMA loads (global_load_lds_dwordx4: no VGPR destination), so a wave carries 8 packets
+// with the VGPR footprint of 4. Issued B first, then A; A is processed from registers, then B's
+// chunks are read back from LDS (each lane reads the 16 bytes it loaded: no bank conflicts).
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int K>
+DEV void row_stage_lds(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
+                       uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint4* wbuf) {
+    const bool valid = p64 < n;
+    const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
+    const bool bad = valid && ((d.off16 < base16) ||
+                               (off + (((uint64_t)d.len + 15u) & ~15ull) > arena_bytes));
+    const bool live = valid && !bad;
+    S.valid = valid;
+    S.bad = bad;
+    S.p = (uint32_t)p64;
+    S.len = live ? d.len : 0u;
+    S.frame = arena + (live ? off : 0);
+    const uint32_t nch = (S.len + 15u) >> 4;
+    const uint4* src = (const uint4*)S.frame;
+    __builtin_amdgcn_global_load_lds((const void*)(rl < nch ? src + rl : &g_zero16), (lds_void_t*)wbuf, 16, 0, 0);
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+        const uint32_t c = rl + 16u * k;
+        const uint4* a = (c < nch) ? src + c : &g_zero16;
+        __builtin_amdgcn_global_load_lds((const void*)a, (lds_void_t*)(wbuf + 64 * k), 16, 0, 2);
+    }
+}
+
+template <int K, int BS, int SF>
+__global__ __launch_bounds__(BS) void update_rows2_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                          const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                          uint32_t base16, uint8_t* __restrict__ status,
+                                                          nfcs_patch* __restrict__ patch,
+                                                          nfcs_patch* __restrict__ ws) {
+    extern __shared__ uint4 lbuf[];
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
+    const uint32_t rowbase4 = (lane & ~15u) * 4u;
+    const uint32_t wv = rfl(threadIdx.x >> 6);
+    const uint64_t pw = (uint64_t)xcd_block() * (BS / 64 * 8) + wv * 8u;
+    if (pw >= n) return;
+    const DescW<8> D = load_descw<8>(desc, pw, n);
+    DescW<4> DA, DB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        DA.w[i] = D.w[i];
+        DB.w[i] = D.w[8 + i];
+    }
+    bool dA = false, dB = false;
+    if (SF == SF_DEFER) {
+        uint32_t sa = 0, sb = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            sa += defer_len(DA.w[2 * i + 1]);
+            sb += defer_len(DB.w[2 * i + 1]);
+        }
+        dA = defer_group(sa, 4);
+        dB = defer_group(sb, 4);
+    }
+    uint4* wbuf = lbuf + wv * (64u * K);
+    RowStage<K> A, B;
+    row_stage_lds<K>(B, arena, arena_bytes, pick_desc<4>(DB, row), pw + 4 + row, n, base16, rl, wbuf);
+    row_stage<K, 16, false>(A, arena, arena_bytes, pick_desc<4>(DA, row), pw + row, n, base16, rl);
+    row_process<K, 16, false>(A, rl, rowbase4, status, patch ? patch : (dA ? ws : nullptr),
+                              SF == SF_INLINE || (SF == SF_DEFER && !dA));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < K; ++k) B.v[k] = wbuf[64 * k + lane];
+    row_process<K, 16, false>(B, rl, rowbase4, status, patch ? patch : (dB ? ws : nullptr),
+                              SF == SF_INLINE || (SF == SF_DEFER && !dB));
+}
 
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
                              uint32_t n, nfcs_patch* ws, unsigned lds_pad, hipStream_t st) {
@@ -41,6 +116,16 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_RECORDS>), g4, dim3(kBlock),
                            lds_pad, st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, ws,
                            (nfcs_patch*)nullptr, nofwd);
+        break;
+    case 6:
+        hipLaunchKernelGGL((update_rows2_kernel<6, 64, SF_DEFER>), dim3((n + 7u) / 8u), dim3(64), 6 * 1024, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        break;
+    case 7:
+        hipLaunchKernelGGL((update_rows2_kernel<6, 256, SF_DEFER>), dim3((n + 31u) / 32u), dim3(256), 24 * 1024,
+                           st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     default: return hipErrorInvalidValue;
     }
