@@ -273,15 +273,16 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
 
 def load_traffic(config: int, n: int, op: str = "update"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), for
-    the default batch size of the config; None otherwise."""
+    the default batch size of the config or, for C1-shaped frames, the 4M-packet C4 shard; None
+    otherwise."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
+    shard = config == 1 and op == "update" and n == 1 << 22
+    if not shard and n != DEFAULT_PACKETS[config]:
+        return None
     try:
-        t = json.load(open(p)).get(f"C{config}" + ("" if op == "update" else f"_{op}"))
+        return json.load(open(p)).get("C4_shard" if shard else f"C{config}" + ("" if op == "update" else f"_{op}"))
     except (OSError, ValueError):
         return None
-    if not t or n != DEFAULT_PACKETS[config]:
-        return None
-    return t
 
 
 def free_port() -> int:
@@ -502,7 +503,7 @@ def main():
     if ws == 1 and args.op == "update" and not args.no_fresh and args.config in (1, 2, 3):
         fresh = fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc)
 
-    traffic = load_traffic(args.config, n, args.op) if (args.align == 128 and ws == 1) else None
+    traffic = load_traffic(args.config, n, args.op) if args.align == 128 else None
     total_packets = D.sum(float(n))
     out = {
         "metric": ("flow keys + hash_flow per second, batched packets, MI355X" if fk else

@@ -30,13 +30,13 @@ KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("upd
           "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_kernel",)}
 
 
-def run_pass(out, cfg, counters, steps, op="update"):
+def run_pass(out, cfg, counters, steps, op="update", packets=0):
     """One rocprofv3 pass with the given counters; per counter, the sum over the op's kernels of
     the median over that kernel's launches."""
-    d = os.path.join(out, f"c{cfg}_{op}_{counters[0]}")
+    d = os.path.join(out, f"c{cfg}{'_' + str(packets) if packets else ''}_{op}_{counters[0]}")
     cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--op", op]
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--op", op] + (["--packets", str(packets)] if packets else [])
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--ops", nargs="+", default=["update"], choices=list(KERNEL))
     ap.add_argument("--merge", help="existing traffic.json to extend")
+    ap.add_argument("--packets", type=int, default=0,
+                    help="packets per launch instead of the config's (C1 with 4194304 = the C4 shard)")
     a = ap.parse_args()
     a.out = os.path.abspath(a.out)  # rocprofv3 runs with cwd /tmp
     os.makedirs(a.out, exist_ok=True)
@@ -73,20 +75,23 @@ def main():
     if a.merge:
         res = json.load(open(a.merge))
     for cfg, op in [(c, o) for o in a.ops for c in a.configs]:
-        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op)
-        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op)
+        P = a.packets
+        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op, P)
+        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op, P)
         q, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
-                        a.steps, op)
-        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op)
+                        a.steps, op, P)
+        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P)
+        key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
+            ("" if op == "update" else f"_{op}")
         fb, wb = 2 * f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
         rq = q["TCC_EA0_RDREQ_sum"]
         rb_req = rq * 128
-        res[f"C{cfg}" + ("" if op == "update" else f"_{op}")] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
-                          "per_packet": (fb + wb) / PACKETS[cfg], "launches": min(nf_, nw),
+        res[key] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+                          "per_packet": (fb + wb) / (P or PACKETS[cfg]), "launches": min(nf_, nw),
                           "read_bytes_from_requests": rb_req, "read_requests": rq,
                           "write_requests": wq["TCC_EA0_WRREQ_sum"],
                           "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}
-        print(f"C{cfg} {op}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
+        print(f"{key} {op}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
               f"{wb / 1e6:.1f} MB in {wq['TCC_EA0_WRREQ_sum']:.0f} requests per launch", flush=True)
     with open(os.path.join(a.out, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
