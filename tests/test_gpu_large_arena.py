@@ -118,10 +118,25 @@ def test_c4_shard_digest_large_arena(engine, rank):
 
 def test_two_streams_share_the_workspace(engine):
     """Back-to-back calls on one context from two streams, no caller patch records: both use the
-    context's deferred-store workspace; the second stream waits for the first's write pass."""
-    import torch
+    context's deferred-store workspace; the second stream waits for the first's write pass. The
+    streams come from the HIP runtime libnfcs.so is linked against (torch bundles its own, which
+    cannot initialise the GPU once this process's engine has)."""
+    import ctypes
+    hip = ctypes.CDLL(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so.7"))
     g = json.load(open(os.path.join(GOLD, "configs.json")))
-    s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+    streams = []
+    for _ in range(2):
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+        streams.append(st)
+
+    class _S:
+        def __init__(self, st):
+            self.cuda_stream = st.value
+
+        def synchronize(self):
+            assert hip.hipStreamSynchronize(ctypes.c_void_p(self.cuda_stream)) == 0
+    s1, s2 = _S(streams[0]), _S(streams[1])
     b1 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
     b2 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
     for _ in range(3):
@@ -138,6 +153,8 @@ def test_two_streams_share_the_workspace(engine):
     for b in (b1, b2):
         b[0].free()
         b[2].free()
+    for st in streams:
+        hip.hipStreamDestroy(st)
 
 
 def test_zero_copy_large_pinned_arena(engine):
