@@ -119,10 +119,10 @@ def test_c4_shard_digest_large_arena(engine, rank):
 def test_two_streams_share_the_workspace(engine):
     """Back-to-back calls on one context from two streams, no caller patch records: both use the
     context's deferred-store workspace; the second stream waits for the first's write pass. The
-    streams come from the HIP runtime libnfcs.so is linked against (torch bundles its own, which
-    cannot initialise the GPU once this process's engine has)."""
+    streams come from the HIP runtime libnfcs.so is bound to: opened by its SONAME, the loader
+    returns the copy already in the process."""
     import ctypes
-    hip = ctypes.CDLL(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so.7"))
+    hip = ctypes.CDLL("libamdhip64.so.7")
     g = json.load(open(os.path.join(GOLD, "configs.json")))
     streams = []
     for _ in range(2):
