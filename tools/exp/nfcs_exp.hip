@@ -13,6 +13,8 @@
 //           5   the read pass only, records for every packet (SF_RECORDS) — no frame writes
 //           6   two row groups per wave, the second landing in LDS (8 packets per wave), 1-wave WGs
 //           7   the same in 256-thread workgroups
+//           9   variant 6's kernel writing patch records only;  10  the same with no writes at all
+//          11   the product's one-wave row kernel with no writes at all
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -82,13 +84,13 @@ __global__ __launch_bounds__(BS) void update_rows2_kernel(uint8_t* __restrict__ 
     RowStage<K> A, B;
     row_stage_lds<K>(B, arena, arena_bytes, pick_desc<4>(DB, row), pw + 4 + row, n, base16, rl, wbuf);
     row_stage<K, 16, false>(A, arena, arena_bytes, pick_desc<4>(DA, row), pw + row, n, base16, rl);
-    row_process<K, 16, false>(A, rl, rowbase4, status, patch ? patch : (dA ? ws : nullptr),
-                              SF == SF_INLINE || (SF == SF_DEFER && !dA));
+    nfcs_patch* recA = SF == 3 ? nullptr : (patch ? patch : (dA ? ws : nullptr));
+    nfcs_patch* recB = SF == 3 ? nullptr : (patch ? patch : (dB ? ws : nullptr));
+    row_process<K, 16, false>(A, rl, rowbase4, status, recA, SF == SF_INLINE || (SF == SF_DEFER && !dA));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < K; ++k) B.v[k] = wbuf[64 * k + lane];
-    row_process<K, 16, false>(B, rl, rowbase4, status, patch ? patch : (dB ? ws : nullptr),
-                              SF == SF_INLINE || (SF == SF_DEFER && !dB));
+    row_process<K, 16, false>(B, rl, rowbase4, status, recB, SF == SF_INLINE || (SF == SF_DEFER && !dB));
 }
 
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
@@ -126,6 +128,19 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((update_rows2_kernel<6, 256, SF_DEFER>), dim3((n + 31u) / 32u), dim3(256), 24 * 1024,
                            st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws);
         hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        break;
+    case 9:  // two-group LDS kernel, records only (frames untouched)
+        hipLaunchKernelGGL((update_rows2_kernel<6, 64, SF_RECORDS>), dim3((n + 7u) / 8u), dim3(64), 6 * 1024, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, ws, (nfcs_patch*)nullptr);
+        break;
+    case 10:  // two-group LDS kernel, no writes at all (bound for full-line record writes)
+        hipLaunchKernelGGL((update_rows2_kernel<6, 64, 3>), dim3((n + 7u) / 8u), dim3(64), 6 * 1024, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, ws, (nfcs_patch*)nullptr);
+        break;
+    case 11:  // product row kernel (one-wave workgroups), no writes at all
+        hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, 64, false, SF_RECORDS>), g1, dim3(64), lds_pad, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr,
+                           (nfcs_patch*)nullptr, nofwd);
         break;
     default: return hipErrorInvalidValue;
     }
