@@ -15,6 +15,8 @@
 //           7   the same in 256-thread workgroups
 //           9   variant 6's kernel writing patch records only;  10  the same with no writes at all
 //          11   the product's one-wave row kernel with no writes at all
+//          12   every packet deferred: records-only read pass + a write pass over every packet
+//          13   that write pass alone (run after 12: it re-applies 12's records)
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -93,6 +95,37 @@ __global__ __launch_bounds__(BS) void update_rows2_kernel(uint8_t* __restrict__ 
     row_process<K, 16, false>(B, rl, rowbase4, status, recB, SF == SF_INLINE || (SF == SF_DEFER && !dB));
 }
 
+// apply_bytes_kernel for every packet (no deferral decision): the write pass of variant 12, where
+// the read pass wrote records for every packet (SF_RECORDS) whatever the frame lengths.
+__global__ __launch_bounds__(kBlock) void apply_all_kernel(uint8_t* __restrict__ arena,
+                                                           const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                           const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool live = i < n;
+    const nfcs_desc d = live ? desc[i] : nfcs_desc{0u, 0u};
+    const uint2 r = live ? ((const uint2*)rec)[i] : make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(live);
+    const uint32_t j = lane & 3u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (((mask >> (16u * k)) & 0xFFFFu) == 0) continue;
+        const int q4 = (int)((16u * k + (lane >> 2)) * 4u);
+        const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.x);
+        const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.y);
+        const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d.off16);
+        const uint32_t ipo = rx & 0xFFFFu, l4o = rx >> 16;
+        const uint32_t off = j < 2 ? ipo : l4o;
+        const uint32_t a = off + (j & 1u);
+        const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+        if (off != NFCS_PATCH_NONE && !overlap) {
+            const uint32_t b = (j < 2 ? (ry >> (8 * j)) : (ry >> (16 + 8 * (j - 2)))) & 0xFFu;
+            uint8_t* p = arena + (uint64_t)o16 * 16u + a;
+            asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");
+        }
+    }
+}
+
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
                              uint32_t n, nfcs_patch* ws, unsigned lds_pad, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
@@ -141,6 +174,14 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, 64, false, SF_RECORDS>), g1, dim3(64), lds_pad, st,
                            arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr,
                            (nfcs_patch*)nullptr, nofwd);
+        break;
+    case 12:  // every packet deferred: records-only read pass (one-wave WGs) + apply_all_kernel
+        hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, 64, false, SF_RECORDS>), g1, dim3(64), lds_pad, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, ws, (nfcs_patch*)nullptr, nofwd);
+        hipLaunchKernelGGL(apply_all_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, ws);
+        break;
+    case 13:  // the write pass alone (records from the last variant-12 call)
+        hipLaunchKernelGGL(apply_all_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, ws);
         break;
     default: return hipErrorInvalidValue;
     }
