@@ -68,16 +68,17 @@ def dist_env():
 
 
 class Dist:
-    """Barrier + max/sum over ranks. torch.distributed (RCCL via backend 'nccl' when GPUs are
-    visible to torch, else gloo); a no-op at world size 1. Only the timing barriers and these
-    reductions cross ranks: the data path has no collective."""
+    """Barrier + max/sum over ranks; a no-op at world size 1. Only the timing barriers and a few
+    scalars cross ranks — the data path has no collective — so they go over gloo
+    on 127.0.0.1 after each rank has synchronised its own GPU: no RCCL communicator, no GPU memory
+    and no xGMI traffic for them. NFCS_DIST_BACKEND=nccl carries them over RCCL instead."""
 
     def __init__(self, ws, rank, local):
         self.ws, self.rank, self.local = ws, rank, local
         if ws > 1:
             import torch
             import torch.distributed as dist
-            backend = os.environ.get("NFCS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            backend = os.environ.get("NFCS_DIST_BACKEND") or "gloo"
             if backend == "nccl":
                 torch.cuda.set_device(local)
             dist.init_process_group(backend=backend)
