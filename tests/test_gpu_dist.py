@@ -1,5 +1,5 @@
 """bench.py's N-rank path on a GPU box, both ranks on cuda:0 here
-(NFCS_BENCH_DEVICE=0; gloo for the timing barriers, since RCCL needs one GPU per rank):
+(NFCS_BENCH_DEVICE=0; the timing barriers go over gloo, bench.py's default):
 (a) `bench.py --gpus 2` with no launcher starts its own two ranks (torch.distributed.run as a child
 process); each owns its own 4M-packet shard of BASELINE config C4 and checks its digest against the
 reference's per-rank C4 digests; rank 0's one JSON line reports n_gpus 2, weak scaling, every rank
@@ -27,8 +27,9 @@ def _free_port():
 
 
 def test_two_ranks_one_gpu_bench_line():
-    env = dict(os.environ, NFCS_BENCH_DEVICE="0", NFCS_DIST_BACKEND="gloo")
+    env = dict(os.environ, NFCS_BENCH_DEVICE="0")  # the default barrier backend (gloo)
     env.pop("WORLD_SIZE", None)
+    env.pop("NFCS_DIST_BACKEND", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
