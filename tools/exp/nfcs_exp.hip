@@ -17,6 +17,8 @@
 //          11   the product's one-wave row kernel with no writes at all
 //          12   every packet deferred: records-only read pass + a write pass over every packet
 //          13   that write pass alone (run after 12: it re-applies 12's records)
+//       14/15   the product's read pass + a write pass of whole 16-byte chunks re-read from the frame
+//               (default-policy / non-temporal re-read)
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -126,6 +128,50 @@ __global__ __launch_bounds__(kBlock) void apply_all_kernel(uint8_t* __restrict__
     }
 }
 
+// Write pass with whole 16-byte chunks (variants 14/15): 4 lanes per deferred packet re-read the
+// frame's first 64 bytes (chunk j by lane j; LD: 0 default policy, 1 non-temporal), patch the
+// checksum bytes in and store the chunks back (`sc0 sc1 nt`), so a 64-byte-aligned frame's write
+// is one whole 64-byte segment instead of a byte-masked partial write. Frames whose fields lie past
+// byte 63, or shorter than 49 bytes, take the byte stores of apply_bytes_kernel.
+template <int LD>
+__global__ __launch_bounds__(kBlock) void apply_seg_kernel(uint8_t* __restrict__ arena,
+                                                           const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                           uint32_t base16, const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u, j = lane & 3u;
+    const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 2;
+    const bool live = p < n;
+    const nfcs_desc d = live ? desc[p] : nfcs_desc{0u, 0u};
+    const uint2 r = live ? ((const uint2*)rec)[p] : make_uint2(0u, 0u);
+    const uint32_t s = row_sum<16>(j == 0 ? defer_len(d.len) : 0u);  // the aligned quad's lengths
+    const bool dfr = live && defer_group(s, 4);
+    if (!dfr) return;
+    const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
+    uint8_t* f = arena + ((uint64_t)d.off16 - base16) * 16u;
+    const bool seg = d.len > 48u && (ipo == NFCS_PATCH_NONE || ipo + 1u < 64u) &&
+                     (l4o == NFCS_PATCH_NONE || l4o + 1u < 64u);
+    if (seg) {
+        uint4* q = (uint4*)f + j;
+        uint4 v = LD ? ld16<1>(q) : *q;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {  // IPv4 bytes first, L4 bytes last (as the reference)
+            const uint32_t off = t < 2 ? ipo : l4o;
+            const uint32_t a = off + (t & 1u);
+            const uint32_t b = (r.y >> (8u * t)) & 0xFFu;
+            if (off != NFCS_PATCH_NONE && (a >> 4) == j) v = put_byte(v, a & 15u, b);
+        }
+        const u32x4_t w = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(q), "v"(w) : "memory");
+    } else {
+        const uint32_t off = j < 2 ? ipo : l4o;
+        const uint32_t a = off + (j & 1u);
+        const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+        if (off != NFCS_PATCH_NONE && !overlap) {
+            const uint32_t b = (r.y >> (8u * j)) & 0xFFu;
+            asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(f + a), "v"(b) : "memory");
+        }
+    }
+}
+
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
                              uint32_t n, nfcs_patch* ws, unsigned lds_pad, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
@@ -183,6 +229,17 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
     case 13:  // the write pass alone (records from the last variant-12 call)
         hipLaunchKernelGGL(apply_all_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, ws);
         break;
+    case 14:
+    case 15: {
+        if (arena_bytes / n < kSmallMeanBytes) NFCS_X(7, 64, g1, SF_DEFER);
+        else hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_DEFER>), g4, dim3(kBlock),
+                                kRowsLdsPad, st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr,
+                                (nfcs_patch*)nullptr, ws, nofwd);
+        const dim3 gs((uint32_t)(((uint64_t)n * 4u + kBlock - 1) / kBlock));
+        if (variant == 14) hipLaunchKernelGGL(apply_seg_kernel<0>, gs, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        else hipLaunchKernelGGL(apply_seg_kernel<1>, gs, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        break;
+    }
     default: return hipErrorInvalidValue;
     }
 #undef NFCS_X
