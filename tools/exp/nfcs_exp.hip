@@ -187,11 +187,11 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
     case 2: NFCS_X(7, 64, g1, SF_INLINE); break;
     case 3:
         NFCS_X(7, 64, g1, SF_DEFER);
-        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel<true>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     case 4:
         NFCS_X(1, kBlock, g4, SF_DEFER);
-        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel<true>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     case 5:
         hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_RECORDS>), g4, dim3(kBlock),
@@ -201,12 +201,12 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
     case 6:
         hipLaunchKernelGGL((update_rows2_kernel<6, 64, SF_DEFER>), dim3((n + 7u) / 8u), dim3(64), 6 * 1024, st,
                            arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws);
-        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel<true>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     case 7:
         hipLaunchKernelGGL((update_rows2_kernel<6, 256, SF_DEFER>), dim3((n + 31u) / 32u), dim3(256), 24 * 1024,
                            st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws);
-        hipLaunchKernelGGL(apply_bytes_kernel, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        hipLaunchKernelGGL(apply_bytes_kernel<true>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     case 9:  // two-group LDS kernel, records only (frames untouched)
         hipLaunchKernelGGL((update_rows2_kernel<6, 64, SF_RECORDS>), dim3((n + 7u) / 8u), dim3(64), 6 * 1024, st,
