@@ -416,6 +416,8 @@ def main():
         done += 1
         if done % 16 == 0:
             eng.sync()
+        if l3 and done % 48 == 0:
+            regen()  # TTL 64: keep every warm-up launch forwarding (an expired packet is not written)
     eng.sync()
     regen()  # l3fwd: fresh TTLs for the timed steps
 
