@@ -36,6 +36,12 @@ enum : int {
 // are latency-bound and hide the inline stores; a mixed batch like C3 (U{64..1500}) lost 3.5% when
 // its waves of mean >= 1024 B (12%) deferred, and defers < 1% of its waves at 1280.
 constexpr uint32_t kDeferMeanBytes = 1280;
+// kUpdateAuto on a burst of at most this many packets stores every wave inline from one kernel:
+// the write pass's launch (~3 µs) outweighs what deferral saves on so few packets (burst sweep,
+// tools/exp/ab.py c<k>n<N>, DESIGN.md §5e: 1K-64K C1 packets 13-35% faster, 64K C3 16%; 64K C2
+// jumbo frames 5% slower; 128K C1 even). The packet count alone decides: the arena size never
+// changes the form.
+constexpr uint32_t kInlineMaxPackets = 65536;
 // Below this mean arena footprint per packet the checksum kernel runs in one-wave workgroups at
 // 7 waves/SIMD (C3 +2-3%); the shape changes speed only, never the store form.
 constexpr uint64_t kSmallMeanBytes = 1200;

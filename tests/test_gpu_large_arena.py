@@ -44,7 +44,7 @@ def apply_patches(arena, desc, pt):
 
 @pytest.mark.parametrize("order", ["arena", "by_length"])
 def test_store_forms_fuzz_vs_oracle(engine, order):
-    frames = oracle.fuzz_frames(30, 0, 60000)
+    frames = oracle.fuzz_frames(30, 0, 90000)  # above kInlineMaxPackets: per-wave forms apply
     if order == "by_length":
         frames = sorted(frames, key=len)
     for align in (16, 128):

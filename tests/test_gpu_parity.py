@@ -154,13 +154,16 @@ def test_edge_cases(engine):
     # VLAN-tagged IPv6 UDP with odd payload; IPv6 jumbo TCP
     frames.append(bytes.fromhex(kat["J_ipv6_vlan_tcp"]["in"]))
     frames.append(bytes.fromhex(kat["I_ipv6_udp_data"]["in"]) + b"x")
-    for align in (16, 64, 4096):
-        arena, desc = oracle.pack_frames(frames, align=align)
+    # alone (a short burst: one inline kernel) and followed by 70,000 64-byte frames (a batch past
+    # kInlineMaxPackets: the waves holding the large frames defer to the write pass)
+    filler = [bytes(base[:64])] * 70000
+    for align, pad in ((16, False), (64, False), (4096, False), (16, True), (128, True)):
+        arena, desc = oracle.pack_frames(frames + (filler if pad else []), align=align)
         ref = arena.copy()
-        rst, _ = oracle.update_batch(ref, desc)
+        rst, _ = oracle.update_batch(ref, desc, nthreads=8)
         out, st, _ = run_device(engine, arena, desc)
-        assert np.array_equal(st, rst), (align, st, rst)
-        assert np.array_equal(out, ref), align
+        assert np.array_equal(st, rst), (align, pad)
+        assert np.array_equal(out, ref), (align, pad)
     # descriptors in reverse / random order (device path accepts any order)
     frames = oracle.fuzz_frames(99, 0, 3000)
     arena, desc = oracle.pack_frames(frames)

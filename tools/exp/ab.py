@@ -7,7 +7,7 @@ batch, whole-arena digest against the reference's (tests/golden/configs.json) wh
 launch re-processes what the previous one just wrote, as on a NIC ring); default 1 = the same
 batch every launch (bench.py's replay). One JSON line per run.
   python tools/exp/ab.py --variants 0,1,4 --work c1,c4shard,c3 [--fresh 4] [--lds 0]
-Work "u<L>": 1M IPv4+UDP frames all of length L (128-byte aligned), built here with numpy (no
+Work "c<k>n<N>": the first N packets of config k (burst-size sweeps). Work "u<L>": 1M IPv4+UDP frames all of length L (128-byte aligned), built here with numpy (no
 reference digest: parity is every variant's output digest equal to variant 0's on the same input).
 """
 import argparse
@@ -57,7 +57,10 @@ def main():
         if w.startswith("u"):
             uniform(eng, int(w[1:]), args, fn)
             continue
-        cfg, n = WORK[w]
+        if w[0] == "c" and "n" in w[1:] and w[1:w.index("n", 1)].isdigit():  # c<k>n<N>: N packets of Ck
+            cfg, n = int(w[1:w.index("n", 1)]), int(w[w.index("n", 1) + 1:])
+        else:
+            cfg, n = WORK[w]
         bs = [eng.config_batch(cfg, SEED, 0, n, 128) for _ in range(args.fresh)]
         ws = eng.alloc(8 * n)
         hd = bs[0][3]
