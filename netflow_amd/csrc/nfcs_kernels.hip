@@ -994,7 +994,9 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     // 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768 vs 0.777, the 4M shard 0.710
     // vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh); one-wave workgroups keep 8.
     const bool small = arena_bytes / n < kSmallMeanBytes;
-    if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;  // short bursts: one kernel
+    // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
+    // launch would cost more than deferral saves on so few packets)
+    if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
     const dim3 g1((n + 3u) / 4u), g4((n + 15u) / 16u);
 #define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
     hipLaunchKernelGGL((update_rows_kernel<6, 16, OCC, BS, false, SF>), G, dim3(BS),                \
