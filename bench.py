@@ -80,7 +80,7 @@ class Dist:
             import torch.distributed as dist
             backend = os.environ.get("NFCS_DIST_BACKEND") or "gloo"
             if backend == "nccl":
-                torch.cuda.set_device(local)
+                torch.cuda.set_device(int(os.environ.get("NFCS_BENCH_DEVICE", local)))
             dist.init_process_group(backend=backend)
             self.dist, self.torch, self.backend = dist, torch, backend
 
@@ -127,13 +127,26 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def device_sync():
+def torch_device_init(device: int) -> bool:
+    """Initialise torch's HIP device BEFORE the engine loads libnfcs.so. The PyTorch-ROCm wheel
+    bundles its own HIP runtime; loaded first, it is the one libnfcs.so binds to (same SONAME), so
+    torch.cuda.synchronize() below sees the engine's work. Loaded after the engine, torch would
+    load a second runtime that finds no GPU."""
     try:
         import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-    except Exception:
-        pass
+    except ImportError:
+        return False
+    if not torch.cuda.is_available():
+        return False
+    torch.cuda.set_device(device)
+    torch.cuda.init()
+    return True
+
+
+def device_sync():
+    """torch.cuda.synchronize() (the bench contract), on the runtime the engine shares."""
+    import torch
+    torch.cuda.synchronize()
 
 
 def shard(rank: int, n_per_rank: int) -> tuple[int, int]:
@@ -353,7 +366,10 @@ def main():
         scaling = "weak"
 
     # NFCS_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a 1-GPU box
-    eng = nf.Engine(int(os.environ.get("NFCS_BENCH_DEVICE", local)))
+    dev = int(os.environ.get("NFCS_BENCH_DEVICE", local))
+    if not torch_device_init(dev):
+        raise SystemExit("bench.py: torch sees no GPU (needs a ROCm GPU for torch.cuda.synchronize)")
+    eng = nf.Engine(dev)
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n, args.align)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
@@ -403,9 +419,9 @@ def main():
         step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
         regen = lambda: None
 
-    # torch (for the synchronize around the timed region) is imported and initialised before
-    # the warm-up: its first import takes ~1.5 s, and an idle GPU between warm-up and timed
-    # region re-enters the timed steps cold (rocprofv3 trace: C3 kernels 0.78 -> 0.99 ms)
+    # torch (for the synchronize around the timed region) was initialised before the engine
+    # (torch_device_init), so nothing slow runs between warm-up and timed region: an idle GPU there
+    # re-enters the timed steps cold (rocprofv3 trace: C3 kernels 0.78 -> 0.99 ms)
     device_sync()
     # untimed warm-up: W steps, continued until --warm-seconds have passed so the timed steps
     # run at the clock the GPU holds under this load (a cold start measured ~4% slower)
