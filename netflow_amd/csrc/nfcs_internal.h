@@ -42,6 +42,15 @@ constexpr uint32_t kDeferMeanBytes = 1280;
 // jumbo frames 5% slower; 128K C1 even). The packet count alone decides: the arena size never
 // changes the form.
 constexpr uint32_t kInlineMaxPackets = 65536;
+// kUpdateAuto on long frames processes a batch of more than kSubBatchAbovePackets as sub-batches
+// of kSubBatchPackets (read pass, then write pass, per sub-batch): 512K header lines (64 MB,
+// 128 MB when frames straddle lines) stay in the 256 MB memory-side cache between the two passes.
+// On the 4M shard 512K and 1M sub-batches measured alike (0.749-0.755 / 0.749 against 0.683-0.714
+// in one launch), 2M 0.710; a 1M batch split in two measured within ±2% of one launch (C1
+// replayed and fresh, two boxes), so batches up to 1M stay one launch (tools/exp/ab.py variants
+// 16-19).
+constexpr uint32_t kSubBatchPackets = 1u << 19;
+constexpr uint32_t kSubBatchAbovePackets = 1u << 20;
 // Below this mean arena footprint per packet the checksum kernel runs in one-wave workgroups at
 // 7 waves/SIMD (C3 +2-3%); the shape changes speed only, never the store form.
 constexpr uint64_t kSmallMeanBytes = 1200;

@@ -977,23 +977,12 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
     }
 }
 
-hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
-                         const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream) {
-    (void)di;
-    if (n == 0) return hipSuccess;
-    if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
-    if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
+// One launch of the checksum path (its read pass and, for kUpdateAuto, its write pass) over n
+// packets, in the workgroup shape `small` chose for the whole call.
+static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
+                                    uint32_t base16, uint8_t* status, nfcs_patch* patch, nfcs_patch* ws,
+                                    int form, bool small, hipStream_t stream) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
-    // Short frames (mean footprint under kSmallMeanBytes per packet) run in one-wave workgroups
-    // held at 7 waves/SIMD: short frames make short-lived waves, and single-wave workgroups retire
-    // and relaunch them with less granularity loss (C3 +2-3%); __launch_bounds__ 7 caps the kernel
-    // at 94 SGPRs (at the compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). The
-    // shape changes speed only: the store form is each wave's own (SF_DEFER).
-    // 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad bytes of (unused) LDS: at the
-    // 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768 vs 0.777, the 4M shard 0.710
-    // vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh); one-wave workgroups keep 8.
-    const bool small = arena_bytes / n < kSmallMeanBytes;
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
@@ -1019,6 +1008,40 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     }
 #undef NFCS_ROWS
     return hipGetLastError();
+}
+
+hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
+                         const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
+                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream) {
+    (void)di;
+    if (n == 0) return hipSuccess;
+    if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
+    if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
+    // Short frames (mean footprint under kSmallMeanBytes per packet) run in one-wave workgroups
+    // held at 7 waves/SIMD: short frames make short-lived waves, and single-wave workgroups retire
+    // and relaunch them with less granularity loss (C3 +2-3%); __launch_bounds__ 7 caps the kernel
+    // at 94 SGPRs (at the compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). The
+    // shape changes speed only: the store form is each wave's own (SF_DEFER).
+    // 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad bytes of (unused) LDS: at the
+    // 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768 vs 0.777, the 4M shard 0.710
+    // vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh); one-wave workgroups keep 8.
+    const bool small = arena_bytes / n < kSmallMeanBytes;
+    // Long frames in a batch of more than kSubBatchAbovePackets: read pass and write pass alternate
+    // per sub-batch of kSubBatchPackets, so the write pass finds its header lines still in the
+    // 256 MB memory-side cache that the read pass just brought them into (the 4M
+    // shard 0.683-0.714 -> 0.749-0.755). Sub-batches are multiples of 4 packets, so every wave's
+    // deferral group is the same as in one launch; they run in order on the stream and share the
+    // workspace.
+    if (form == kUpdateAuto && !small && n > kSubBatchAbovePackets) {
+        for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
+            const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(kSubBatchPackets, n - i),
+                                                   base16, status ? status + i : nullptr,
+                                                   patch ? patch + i : nullptr, ws, form, small, stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, small, stream);
 }
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,

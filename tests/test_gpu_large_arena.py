@@ -173,3 +173,33 @@ def test_zero_copy_large_pinned_arena(engine):
         assert np.array_equal(pinned, src)
     finally:
         engine.host_free(pinned)
+
+
+def test_sub_batches_status_patch_and_digest(engine):
+    """A long-frame batch past kSubBatchAbovePackets (1.5M C1-shaped packets from index 12,345:
+    sub-batches of 512K, 512K and 476K): statuses and caller patch records land at their packets'
+    own indices, the status histogram and result digest equal the oracle's (pinned to the
+    reference), and every record names the bytes now in its frame."""
+    g = json.load(open(os.path.join(GOLD, "configs.json")))
+    n, first = 1_500_000, 12_345
+    d_arena, nbytes, d_desc, hdesc = engine.config_batch(1, g["seed"], first, n, 128)
+    din, dout, hist = oracle.config_digest(1, g["seed"], first, n, 8)
+    assert engine.digest_device(d_arena, nbytes, d_desc, n, first) == din
+    d_st, d_pt = engine.alloc(n), engine.alloc(8 * n)
+    engine.update_device(d_arena, nbytes, d_desc, n, d_st, d_pt)
+    engine.sync()
+    assert engine.digest_device(d_arena, nbytes, d_desc, n, first) == dout
+    st = d_st.download(np.uint8, n)
+    vals, cnt = np.unique(st, return_counts=True)
+    assert {int(v): int(c) for v, c in zip(vals, cnt)} == hist
+    pt = d_pt.download(nf.PATCH_DTYPE, n)
+    arena = d_arena.download(np.uint8, nbytes)
+    base = hdesc["off16"].astype(np.int64) * 16
+    for f in ("ip", "l4"):
+        off = pt[f + "_off"].astype(np.int64)
+        live = off != 0xFFFF
+        assert live.all()  # every C1 packet has both fields
+        for b in (0, 1):
+            assert np.array_equal(arena[base[live] + off[live] + b], pt[f][live, b])
+    for b in (d_arena, d_desc, d_st, d_pt):
+        b.free()

@@ -19,6 +19,8 @@
 //          13   that write pass alone (run after 12: it re-applies 12's records)
 //       14/15   the product's read pass + a write pass of whole 16-byte chunks re-read from the frame
 //               (default-policy / non-temporal re-read)
+//    16/17/18   the product form over consecutive sub-batches of 1M / 512K / 2M packets (the
+//               product itself uses 512K, kSubBatchPackets);  19  one launch pair, no sub-batches
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -240,6 +242,20 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         else hipLaunchKernelGGL(apply_seg_kernel<1>, gs, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     }
+    case 16:
+    case 17:
+    case 18: {  // the product form over consecutive sub-batches of 1M / 512K / 2M packets
+        const uint32_t S = variant == 16 ? (1u << 20) : (variant == 17 ? (1u << 19) : (1u << 21));
+        for (uint32_t i = 0; i < n; i += S) {
+            const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(S, n - i), 0u, nullptr,
+                                                   nullptr, ws, kUpdateAuto, arena_bytes / n < kSmallMeanBytes, st);
+            if (e != hipSuccess) return e;
+        }
+        break;
+    }
+    case 19:  // the product form in ONE launch pair (no sub-batches), the round-2 session-1/2 form
+        return launch_update_one(arena, arena_bytes, desc, n, 0u, nullptr, nullptr, ws, kUpdateAuto,
+                                 arena_bytes / n < kSmallMeanBytes, st);
     default: return hipErrorInvalidValue;
     }
 #undef NFCS_X
