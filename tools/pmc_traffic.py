@@ -83,11 +83,19 @@ def main():
         wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P)
         key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
             ("" if op == "update" else f"_{op}")
+        # launches per call: nfcs_update_device runs a long-frame batch of more than 1M packets
+        # as 512K-packet sub-batches (kSubBatchPackets), each its own read pass + write pass
+        sub = -(-P // (1 << 19)) if (op == "update" and P > (1 << 20)) else 1
+        f = {k: v * sub for k, v in f.items()}
+        w = {k: v * sub for k, v in w.items()}
+        q = {k: v * sub for k, v in q.items()}
+        wq = {k: v * sub for k, v in wq.items()}
         fb, wb = 2 * f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
         rq = q["TCC_EA0_RDREQ_sum"]
         rb_req = rq * 128
         res[key] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                           "per_packet": (fb + wb) / (P or PACKETS[cfg]), "launches": min(nf_, nw),
+                    "launches_per_call": sub,
                           "read_bytes_from_requests": rb_req, "read_requests": rq,
                           "write_requests": wq["TCC_EA0_WRREQ_sum"],
                           "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}
