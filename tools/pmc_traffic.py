@@ -100,7 +100,7 @@ def main():
                           "write_requests": wq["TCC_EA0_WRREQ_sum"],
                           "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}
         print(f"{key} {op}: read {fb / 1e9:.3f} GB (requests: {rb_req / 1e9:.3f} GB)  write "
-              f"{wb / 1e6:.1f} MB in {wq["TCC_EA0_WRREQ_sum"]:.0f} requests per call", flush=True)
+              f"{wb / 1e6:.1f} MB in {wq['TCC_EA0_WRREQ_sum']:.0f} requests per call", flush=True)
     with open(os.path.join(a.out, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
 
