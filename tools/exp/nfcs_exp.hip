@@ -21,6 +21,7 @@
 //               (default-policy / non-temporal re-read)
 //    16/17/18   the product form over consecutive sub-batches of 1M / 512K / 2M packets (the
 //               product itself uses 512K, kSubBatchPackets);  19  one launch pair, no sub-batches
+//       20/21   256K / 512K sub-batches with write pass i on a second stream, overlapping read pass i+1
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -256,6 +257,34 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
     case 19:  // the product form in ONE launch pair (no sub-batches), the round-2 session-1/2 form
         return launch_update_one(arena, arena_bytes, desc, n, 0u, nullptr, nullptr, ws, kUpdateAuto,
                                  arena_bytes / n < kSmallMeanBytes, st);
+    case 20:
+    case 21: {  // sub-batches of 256K (20) / 512K (21): read pass i+1 overlaps write pass i on a second stream
+        static hipStream_t s2 = nullptr;
+        static hipEvent_t ev[64];
+        if (!s2) {
+            if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return hipErrorInvalidValue;
+            for (auto& x : ev) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+        }
+        const uint32_t S = variant == 20 ? (1u << 18) : (1u << 19);
+        const bool small = arena_bytes / n < kSmallMeanBytes;
+        int k = 0;
+        for (uint32_t i = 0; i < n && k < 63; i += S, ++k) {
+            const uint32_t m = std::min(S, n - i);
+            if (small) hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, 64, false, SF_DEFER>), dim3((m + 3u) / 4u),
+                                          dim3(64), 0u, st, arena, arena_bytes, desc + i, m, 0u, (uint8_t*)nullptr,
+                                          (nfcs_patch*)nullptr, ws + i, nofwd);
+            else hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_DEFER>), dim3((m + 15u) / 16u),
+                                    dim3(kBlock), kRowsLdsPad, st, arena, arena_bytes, desc + i, m, 0u,
+                                    (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws + i, nofwd);
+            (void)hipEventRecord(ev[k], st);
+            (void)hipStreamWaitEvent(s2, ev[k], 0);
+            hipLaunchKernelGGL(apply_bytes_kernel<true>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, s2,
+                               arena, desc + i, m, 0u, ws + i);
+        }
+        (void)hipEventRecord(ev[63], s2);
+        (void)hipStreamWaitEvent(st, ev[63], 0);  // the call ends when its last write pass has
+        break;
+    }
     default: return hipErrorInvalidValue;
     }
 #undef NFCS_X
