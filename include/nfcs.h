@@ -136,7 +136,10 @@ NFCS_API int nfcs_ctx_host_numa(nfcs_ctx* ctx, int* node, int* local);
  *   d_status     optional (NULL) n status bytes, NFCS_ST_*
  *   d_patch      optional (NULL) n nfcs_patch records describing the bytes written
  *   stream       hipStream_t or NULL (context stream). Asynchronous: completion is
- *                observed by synchronising the stream. */
+ *                observed by synchronising the stream.
+ * Launches (speed only; the bytes written never depend on them): a call of at most 65,536
+ * packets is one kernel; waves of long frames write their checksum bytes in a second, write-only
+ * pass; a long-frame call of more than 1M packets runs as consecutive 512K-packet sub-batches. */
 NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                 nfcs_patch* d_patch, void* stream);
