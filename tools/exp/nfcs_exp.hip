@@ -22,6 +22,7 @@
 //    16/17/18   the product form over consecutive sub-batches of 1M / 512K / 2M packets (the
 //               product itself uses 512K, kSubBatchPackets);  19  one launch pair, no sub-batches
 //       20/21   256K / 512K sub-batches with write pass i on a second stream, overlapping read pass i+1
+//       22/23   the product's launches (long-frame shape) with the write pass's stores plain / sc1
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -175,6 +176,44 @@ __global__ __launch_bounds__(kBlock) void apply_seg_kernel(uint8_t* __restrict__
     }
 }
 
+// apply_bytes_kernel<true> with another store policy (variants 22/23): POL 0 plain (write-back),
+// 1 `sc1` (agent-scope write-through). The product stores `sc0 sc1 nt`.
+template <int POL>
+__global__ __launch_bounds__(kBlock) void apply_pol_kernel(uint8_t* __restrict__ arena,
+                                                           const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                           const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
+    const uint2 r0 = i < n ? ((const uint2*)rec)[i] : make_uint2(0u, 0u);
+    uint32_t s = defer_len(d.len);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);
+    const bool dfr = i < n && defer_group(s, 4);
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(dfr);
+    if (!mask) return;
+    const uint2 r = dfr ? r0 : make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
+    const uint32_t j = lane & 3u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (((mask >> (16u * k)) & 0xFFFFu) == 0) continue;
+        const int q4 = (int)((16u * k + (lane >> 2)) * 4u);
+        const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.x);
+        const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.y);
+        const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d.off16);
+        const uint32_t ipo = rx & 0xFFFFu, l4o = rx >> 16;
+        const uint32_t off = j < 2 ? ipo : l4o;
+        const uint32_t a = off + (j & 1u);
+        const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+        if (off != NFCS_PATCH_NONE && !overlap) {
+            const uint32_t b = (j < 2 ? (ry >> (8 * j)) : (ry >> (16 + 8 * (j - 2)))) & 0xFFu;
+            uint8_t* p = arena + (uint64_t)o16 * 16u + a;
+            if (POL == 1) st8<true>(p, b);
+            else *p = (uint8_t)b;
+        }
+    }
+}
+
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
                              uint32_t n, nfcs_patch* ws, unsigned lds_pad, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
@@ -283,6 +322,23 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         }
         (void)hipEventRecord(ev[63], s2);
         (void)hipStreamWaitEvent(st, ev[63], 0);  // the call ends when its last write pass has
+        break;
+    }
+    case 22:
+    case 23: {  // the product's sub-batched launches with the write pass's stores plain (22) / sc1 (23)
+        const uint32_t S = n > kSubBatchAbovePackets ? kSubBatchPackets : n;
+        for (uint32_t i = 0; i < n; i += S) {
+            const uint32_t m = std::min(S, n - i);
+            hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_DEFER>), dim3((m + 15u) / 16u),
+                               dim3(kBlock), kRowsLdsPad, st, arena, arena_bytes, desc + i, m, 0u, (uint8_t*)nullptr,
+                               (nfcs_patch*)nullptr, ws, nofwd);
+            if (variant == 22)
+                hipLaunchKernelGGL(apply_pol_kernel<0>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, st, arena,
+                                   desc + i, m, ws);
+            else
+                hipLaunchKernelGGL(apply_pol_kernel<1>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, st, arena,
+                                   desc + i, m, ws);
+        }
         break;
     }
     default: return hipErrorInvalidValue;
