@@ -116,6 +116,11 @@ NFCS_API int nfcs_abi_version(void);
 NFCS_API const char* nfcs_strerror(int err);
 NFCS_API int nfcs_last_hip_error(void);
 
+/* Threads: any entry point may be called from any host thread; it makes the context's device
+ * current for its duration and restores the caller's device on return. Calls on ONE context are
+ * serialised by the caller (or ordered by a stream); different contexts run concurrently
+ * (netflow_amd::MultiGpu, include/netflow_amd/multi_gpu.hpp: one thread per GPU). */
+
 /* One context per device: owns a stream, events and the pinned staging ring used by
  * nfcs_update_host. Calls on one context must be serialised by the caller. */
 NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out);

@@ -110,6 +110,22 @@ int hip_fail(hipError_t e) {
 
 hipStream_t pick(nfcs_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
+// Makes `device` current on the calling thread for one entry point and restores the caller's
+// device on return: a context may be driven from any host thread (netflow_amd::MultiGpu runs one
+// thread per GPU), and allocations / copies must land on the context's device.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+        else prev = -1;  // nothing to restore
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 // The GPU's NUMA node from sysfs (PCI bus id -> /sys/bus/pci/devices/<id>/numa_node), -1 if unknown.
 int gpu_numa_node(int device) {
     char bus[64] = {0};
@@ -343,7 +359,8 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
         (void)hipGetLastError();
         return NFCS_ENODEV;
     }
-    NFCS_HIP(hipSetDevice(device));
+    DeviceGuard dg_(device);  // the new context's device while it is set up; the caller's after
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipDeviceProp_t prop;
     NFCS_HIP(hipGetDeviceProperties(&prop, device));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NFCS_ENODEV;
@@ -367,7 +384,7 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
 
 NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     if (!c) return NFCS_OK;
-    (void)hipSetDevice(c->di.device);
+    DeviceGuard dg_(c->di.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
@@ -403,6 +420,8 @@ NFCS_API int nfcs_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_by
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                 nfcs_patch* d_patch, void* stream) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     return update_device(c, d_arena, arena_bytes, d_desc, n, d_status, d_patch, pick(c, stream));
@@ -413,6 +432,8 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
                                     const nfcs_nexthop* d_table, uint32_t table_n,
                                     uint8_t* d_status, void* stream) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || !d_nh || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (table_n > 0 && (!d_table || ((uintptr_t)d_table & 3u))) return NFCS_EINVAL;
@@ -426,6 +447,8 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
                               uint32_t op_all, const uint32_t* d_caps, uint32_t cap_all,
                               uint8_t* d_status, void* stream) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
@@ -438,6 +461,8 @@ NFCS_API int nfcs_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t
                                    const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
                                    uint32_t* d_hash, void* stream) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u) || ((uintptr_t)d_keys & 15u))
         return NFCS_EINVAL;
@@ -450,6 +475,8 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                               const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
                               uint32_t flags) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!h_arena || !h_desc) return NFCS_EINVAL;
     // Checked before anything is queued: frames in arena order, and every frame that lies inside
@@ -624,6 +651,8 @@ NFCS_API int nfcs_gen_config_device(nfcs_ctx* c, int config, uint64_t seed, uint
                                     uint32_t n, uint8_t* d_arena, uint64_t arena_bytes,
                                     const nfcs_desc* d_desc, void* stream) {
     if (!c || config < 0 || config > 3) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc) return NFCS_EINVAL;
     // padding between aligned frame starts is zeroed too, so the arena is fully defined
@@ -637,6 +666,8 @@ NFCS_API int nfcs_digest_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t ar
                                 const nfcs_desc* d_desc, uint32_t n, uint64_t first,
                                 uint64_t* h_digest, void* stream) {
     if (!c || !h_digest) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipMemsetAsync(c->d_digest, 0, sizeof(uint64_t), st));
     if (n) {
@@ -650,7 +681,8 @@ NFCS_API int nfcs_digest_device(nfcs_ctx* c, const uint8_t* d_arena, uint64_t ar
 
 NFCS_API int nfcs_device_alloc(nfcs_ctx* c, size_t bytes, void** out) {
     if (!c || !out) return NFCS_EINVAL;
-    NFCS_HIP(hipSetDevice(c->di.device));
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipError_t e = hipMalloc(out, bytes ? bytes : 16);
     if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return NFCS_ENOMEM; }
     NFCS_HIP(e);
@@ -658,11 +690,15 @@ NFCS_API int nfcs_device_alloc(nfcs_ctx* c, size_t bytes, void** out) {
 }
 NFCS_API int nfcs_device_free(nfcs_ctx* c, void* p) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     NFCS_HIP(hipFree(p));
     return NFCS_OK;
 }
 NFCS_API int nfcs_host_alloc(nfcs_ctx* c, size_t bytes, void** out) {
     if (!c || !out) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipError_t e = hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault);
     if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return NFCS_ENOMEM; }
     NFCS_HIP(e);
@@ -670,23 +706,31 @@ NFCS_API int nfcs_host_alloc(nfcs_ctx* c, size_t bytes, void** out) {
 }
 NFCS_API int nfcs_host_free(nfcs_ctx* c, void* p) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     NFCS_HIP(hipHostFree(p));
     return NFCS_OK;
 }
 NFCS_API int nfcs_memcpy_h2d(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     NFCS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     NFCS_HIP(hipStreamSynchronize(c->stream));
     return NFCS_OK;
 }
 NFCS_API int nfcs_memcpy_d2h(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     NFCS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     NFCS_HIP(hipStreamSynchronize(c->stream));
     return NFCS_OK;
 }
 NFCS_API int nfcs_stream_sync(nfcs_ctx* c, void* stream) {
     if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     NFCS_HIP(hipStreamSynchronize(pick(c, stream)));
     return NFCS_OK;
 }
@@ -696,6 +740,8 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     NFCS_HIP(hipEventRecord(c->ev0, st));
@@ -714,6 +760,8 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
                                          uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
                                          uint8_t* d_status, int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0 || !d_arena || !d_desc || !d_nh) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
@@ -730,6 +778,8 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
                                    uint32_t op_alt, uint32_t cap_all, uint8_t* d_status, int iters,
                                    void* stream, float* ms) {
     if (!c || !ms || iters <= 0 || !d_arena || !d_desc) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
@@ -745,6 +795,8 @@ NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uin
                                         const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
                                         uint32_t* d_hash, int iters, void* stream, float* ms) {
     if (!c || !ms || iters <= 0 || !d_arena || !d_desc) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)

@@ -7,11 +7,17 @@
 //             `room` bytes from the data start; prints "<ok> <status> <new len> <hex of room
 //             bytes from the data start>" per frame
 //   vlan1   : same through Packet::push_vlan / pop_vlan one packet at a time (host CPU)
+//   multi K : the frames packed into one host arena (128-byte slots) and updated by
+//             netflow_amd::MultiGpu over K contexts on device 0 (one host thread each); prints
+//             "<status> <hex>" per frame, then "bounds b0 b1 ... bK" on stderr
+#include <netflow_amd/multi_gpu.hpp>
 #include <netflow_amd/packet.hpp>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <iostream>
 #include <string>
 #include <vector>
@@ -247,6 +253,37 @@ static int pool_bench() {
     return 0;
 }
 
+// MultiGpu over K contexts (all on device 0 here: the one-GPU box rehearses the per-GPU threads,
+// staging rings and byte-balanced ranges of an 8-GPU node).
+static int multi_mode(int k) {
+    std::vector<std::vector<uint8_t>> fr;
+    std::string line;
+    while (std::getline(std::cin, line)) fr.push_back(unhex(line));
+    std::vector<nfcs_desc> desc(fr.size());
+    uint64_t off = 0;
+    for (size_t i = 0; i < fr.size(); ++i) {
+        desc[i].off16 = (uint32_t)(off / 16);
+        desc[i].len = (uint32_t)fr[i].size();
+        off += (fr[i].size() + 127) / 128 * 128;
+    }
+    std::vector<uint8_t> arena(off + 16, 0);
+    for (size_t i = 0; i < fr.size(); ++i)
+        if (!fr[i].empty()) std::memcpy(arena.data() + (uint64_t)desc[i].off16 * 16, fr[i].data(), fr[i].size());
+    int rc = 0;
+    netflow_amd::MultiGpu mg(std::vector<int>(k, 0), std::nothrow, &rc);
+    if (rc) { std::fprintf(stderr, "ctx rc=%d\n", rc); return 2; }
+    std::vector<uint8_t> st(fr.size(), 0xEE);
+    std::vector<uint32_t> b(k + 1);
+    rc = mg.update_host(arena.data(), arena.size(), desc.data(), (uint32_t)fr.size(), st.data(), 0, b.data());
+    if (rc) { std::fprintf(stderr, "rc=%d\n", rc); return 3; }
+    for (size_t i = 0; i < fr.size(); ++i)
+        std::printf("%d %s\n", (int)st[i], hex(arena.data() + (uint64_t)desc[i].off16 * 16, fr[i].size()).c_str());
+    std::fprintf(stderr, "bounds");
+    for (uint32_t x : b) std::fprintf(stderr, " %u", x);
+    std::fprintf(stderr, "\n");
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (mode == "poolbench") return pool_bench();
@@ -256,6 +293,7 @@ int main(int argc, char** argv) {
     if (mode == "vlan" || mode == "vlan1") return vlan_mode(mode == "vlan1");
     if (mode == "l3") return l3_mode();
     if (mode == "flow") return flow_mode();
+    if (mode == "multi") return multi_mode(argc > 2 ? std::atoi(argv[2]) : 2);
     std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> bufs;
     std::vector<std::unique_ptr<netflow_amd::Packet>> pkts;
     std::string line;

@@ -171,3 +171,30 @@ def test_cpp_api_host_code_under_asan_ubsan():
     r = subprocess.run([exe, "cpu"], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode in (0,) and "api_failures=0" in r.stdout, r.stdout + r.stderr[-3000:]
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [2, 3])
+def test_cpp_multi_gpu_host_burst_matches_oracle(exe, k):
+    """netflow_amd::MultiGpu (include/netflow_amd/multi_gpu.hpp, SURVEY.md §8e): one host burst
+    split by frame bytes over k contexts (all on device 0 here), one host thread and one staging
+    ring each; every frame bit-exact with the oracle, statuses at their own indices, the ranges
+    tiling the burst within one frame of byte balance."""
+    frames = _frames()
+    r = subprocess.run([exe, "multi", str(k)], input="\n".join(f.hex() for f in frames) + "\n",
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(frames)
+    for f, line in zip(frames, lines):
+        st, hx = (line.split(" ") + [""])[:2]
+        exp, est = oracle.update_frame(f)
+        if (est & 0x3F) == 14:
+            assert hx == f.hex()
+            continue
+        assert hx == exp.hex()
+        assert int(st) == est
+    b = [int(x) for x in r.stderr.strip().split("bounds", 1)[1].split()]
+    assert len(b) == k + 1 and b[0] == 0 and b[-1] == len(frames) and b == sorted(b)
+    per = [sum(len(f) for f in frames[b[p]:b[p + 1]]) for p in range(k)]
+    assert max(per) - min(per) <= 2 * max(len(f) for f in frames)
