@@ -175,13 +175,15 @@ def test_zero_copy_large_pinned_arena(engine):
         engine.host_free(pinned)
 
 
-def test_sub_batches_status_patch_and_digest(engine):
-    """A long-frame batch past kSubBatchAbovePackets (1.5M C1-shaped packets from index 12,345:
-    sub-batches of 512K, 512K and 476K): statuses and caller patch records land at their packets'
-    own indices, the status histogram and result digest equal the oracle's (pinned to the
-    reference), and every record names the bytes now in its frame."""
+@pytest.mark.parametrize("n", [1_500_000, 2 * 524_288 + 100])
+def test_sub_batches_status_patch_and_digest(engine, n):
+    """A long-frame batch past kSubBatchAbovePackets (C1-shaped packets from index 12,345: 1.5M =
+    sub-batches of 512K, 512K and 476K; 1M + 100 = 512K, 512K and a 100-packet tail that runs as
+    one inline kernel): statuses and caller patch records land at their packets' own indices, the
+    status histogram and result digest equal the oracle's (pinned to the reference), and every
+    record names the bytes now in its frame."""
     g = json.load(open(os.path.join(GOLD, "configs.json")))
-    n, first = 1_500_000, 12_345
+    first = 12_345
     d_arena, nbytes, d_desc, hdesc = engine.config_batch(1, g["seed"], first, n, 128)
     din, dout, hist = oracle.config_digest(1, g["seed"], first, n, 8)
     assert engine.digest_device(d_arena, nbytes, d_desc, n, first) == din
