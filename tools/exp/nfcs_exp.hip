@@ -366,3 +366,72 @@ extern "C" NFCS_API int nfcs_exp_time_update(int variant, uint8_t* d_arena, uint
     (void)hipEventDestroy(e1);
     return (int)e;
 }
+
+// ---- flow keys: launch forms (nfcs_exp_time_flow) -------------------------------------------
+//   variant 0   the product (launch_flow_keys: one wave per 32 packets, XCD-aware block order)
+//           1/2 a persistent grid (1/2: CUs x 8 / CUs x 16 workgroups of 256 threads) striding over
+//               the same 32-packet wave groups, so the launch has no ramp-up / drain of short waves
+namespace nfcs {
+template <int K>
+__global__ __launch_bounds__(kBlock) void flow_keys_loop_kernel(const uint8_t* __restrict__ arena,
+                                                                uint64_t arena_bytes,
+                                                                const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                                nfcs_flow_key* __restrict__ keys,
+                                                                uint32_t* __restrict__ hashes) {
+    constexpr int R = 8;
+    constexpr uint32_t PR = 64 / R, PW = PR * K;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t groups = ((uint64_t)n + PW - 1) / PW;
+    const uint64_t stride = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + rfl(threadIdx.x >> 6); w < groups; w += stride) {
+        const uint64_t pw = w * PW;
+        uint2 dl = make_uint2(0u, 0u);
+        if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
+        uint4 c[K];
+        uint32_t L[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t sl = (uint32_t)k * PR + row;
+            const uint32_t off16 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.x);
+            const uint32_t dlen = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.y);
+            const uint64_t off = (uint64_t)off16 * 16u;
+            const bool live = pw + sl < n && off + (((uint64_t)dlen + 15u) & ~15ull) <= arena_bytes;
+            L[k] = live ? dlen : 0u;
+            const uint4* src = (const uint4*)(arena + (live ? off : 0));
+            c[k] = ld16<0>((rl * 16u < L[k]) ? src + rl : &g_zero16);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            flow_key_row(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
+    }
+}
+}  // namespace nfcs
+
+extern "C" NFCS_API int nfcs_exp_time_flow(int variant, const uint8_t* d_arena, uint64_t arena_bytes,
+                                          const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,
+                                          uint32_t* d_hash, int iters, void* stream, float* ms) {
+    hipStream_t st = (hipStream_t)stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return -1;
+    const unsigned cus = (unsigned)prop.multiProcessorCount;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1;
+    hipError_t e = hipEventRecord(e0, st);
+    for (int it = 0; it < iters && e == hipSuccess; ++it) {
+        if (variant == 0) {
+            e = nfcs::launch_flow_keys(nfcs::DevInfo{}, d_arena, arena_bytes, d_desc, n, d_keys, d_hash, st);
+        } else {
+            const unsigned g = cus * (variant == 1 ? 8u : 16u);
+            hipLaunchKernelGGL((nfcs::flow_keys_loop_kernel<4>), dim3(g), dim3(nfcs::kBlock), 0, st, d_arena,
+                               arena_bytes, d_desc, n, d_keys, d_hash);
+            e = hipGetLastError();
+        }
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return (int)e;
+}
