@@ -56,8 +56,13 @@ public:
         if (rc != NFCS_OK) return rc;
         std::vector<int> res(parts, NFCS_OK);
         std::vector<std::thread> th;
-        for (uint32_t p = 1; p < parts; ++p)
-            th.emplace_back([&, p] { res[p] = run(p, b, h_arena, arena_bytes, h_desc, h_status, flags); });
+        for (uint32_t p = 1; p < parts; ++p) {
+            try {
+                th.emplace_back([&, p] { res[p] = run(p, b, h_arena, arena_bytes, h_desc, h_status, flags); });
+            } catch (...) {  // no thread to be had: run that range here, in turn (never throw)
+                res[p] = run(p, b, h_arena, arena_bytes, h_desc, h_status, flags);
+            }
+        }
         res[0] = run(0, b, h_arena, arena_bytes, h_desc, h_status, flags);
         for (auto& t : th) t.join();
         if (bounds)
