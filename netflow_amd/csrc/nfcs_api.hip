@@ -218,10 +218,15 @@ void par_memcpy(void* dst, const void* src, size_t bytes, int threads, const cpu
     for (size_t i = 1; i < t; ++i) {
         const size_t o = i * per;
         if (o >= bytes) break;
-        th.emplace_back([=] {
+        auto part = [=] {
             if (cpus) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), cpus);
             memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
-        });
+        };
+        try {
+            th.emplace_back(part);
+        } catch (...) {  // no thread to be had: copy this part here (nothing throws across the ABI)
+            memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
+        }
     }
     memcpy(dst, src, std::min(per, bytes));
     for (auto& x : th) x.join();
