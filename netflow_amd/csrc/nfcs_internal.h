@@ -54,6 +54,10 @@ constexpr uint32_t kSubBatchAbovePackets = 1u << 20;
 // Below this mean arena footprint per packet the checksum kernel runs in one-wave workgroups at
 // 7 waves/SIMD (C3 +2-3%); the shape changes speed only, never the store form.
 constexpr uint64_t kSmallMeanBytes = 1200;
+// Below this one it runs 8-lane rows, 8 packets per wave (short frames are packet-rate bound:
+// uniform 64-256 B frames 1.8-1.9x, IMIX 7:4:1 of 64/570/1500 B 1.47x, 768 B 1.2x; the C3 mix,
+// 870 B of footprint per packet, stays on 16-lane rows, where 8-lane rows lose 7.5%).
+constexpr uint64_t kTinyMeanBytes = 800;
 // Dynamic LDS per 256-thread checksum workgroup (unused): 6 workgroups = 6 waves/SIMD per CU.
 constexpr unsigned kRowsLdsPad = 24576;
 

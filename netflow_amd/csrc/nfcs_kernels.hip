@@ -907,13 +907,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
             wmac[3 * i + 2] = m[2];
         }
     }
-    // the wave's store form, from its own frame lengths (scalar arithmetic on the descriptors)
+    // the store form of each aligned group of 4 packets, from their own frame lengths (scalar
+    // arithmetic on the descriptors): the whole wave with 16-lane rows, each half of the wave with
+    // 8-lane rows; apply_bytes_kernel recomputes the same groups
     bool defer = false;
     if (SF == SF_DEFER) {
-        uint32_t s = 0;
+        static_assert(PW == 4 || PW == 8, "deferral groups of 4 packets");
+        uint32_t s0 = 0, s1 = 0;
 #pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) s += defer_len(D.w[2 * i + 1]);
-        defer = defer_group(s, PW);
+        for (uint32_t i = 0; i < 4; ++i) s0 += defer_len(D.w[2 * i + 1]);
+#pragma unroll
+        for (uint32_t i = 4; i < PW; ++i) s1 += defer_len(D.w[2 * i + 1]);
+        defer = (PW == 8 && row >= 4) ? defer_group(s1, 4) : defer_group(s0, 4);
     }
     const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
     nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
@@ -977,35 +982,55 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
     }
 }
 
+// Workgroup shapes of the checksum read pass, chosen per call from the mean arena footprint per
+// packet (speed only: results and store forms never depend on it):
+//   kShapeTiny   (< kTinyMeanBytes)  8-lane rows of 6 slots (768 B per row pass), 8 packets per
+//                one-wave workgroup: frames this short are packet-rate bound, and twice the packets
+//                per wave doubles it (64-256 B frames 1.8-1.9x, IMIX 1.47x, 768 B 1.2x);
+//   kShapeShort  (< kSmallMeanBytes) 16-lane rows in one-wave workgroups at 7 waves/SIMD: mixes of
+//                short and long frames (C3), where 8-lane rows would need a second row pass for
+//                most waves (C3 -7.5%);
+//   kShapeLong   16-lane rows in 256-thread workgroups held at 6 waves/SIMD.
+enum : int { kShapeTiny = 0, kShapeShort = 1, kShapeLong = 2 };
+
 // One launch of the checksum path (its read pass and, for kUpdateAuto, its write pass) over n
-// packets, in the workgroup shape `small` chose for the whole call.
+// packets, in the shape chosen for the whole call.
 static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
                                     uint32_t base16, uint8_t* status, nfcs_patch* patch, nfcs_patch* ws,
-                                    int form, bool small, hipStream_t stream) {
+                                    int form, int shape, hipStream_t stream) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
-    const dim3 g1((n + 3u) / 4u), g4((n + 15u) / 16u);
+    const dim3 g8((n + 7u) / 8u), g1((n + 3u) / 4u), g4((n + 15u) / 16u);
 #define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
     hipLaunchKernelGGL((update_rows_kernel<6, 16, OCC, BS, false, SF>), G, dim3(BS),                \
                        BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc, n, base16,  \
                        status, patch, ws, nofwd)
+#define NFCS_ROWS8(SF)                                                                             \
+    hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, false, SF>), g8, dim3(64), 0u, stream, arena,  \
+                       arena_bytes, desc, n, base16, status, patch, ws, nofwd)
+#define NFCS_SHAPED(SF)                                                                            \
+    do {                                                                                           \
+        if (shape == kShapeTiny) NFCS_ROWS8(SF);                                                   \
+        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);                                   \
+        else NFCS_ROWS(1, kBlock, g4, SF);                                                         \
+    } while (0)
     if (form == kUpdateRecords) {
         NFCS_ROWS(1, kBlock, g4, SF_RECORDS);
     } else if (form == kUpdateInline) {
-        if (small) NFCS_ROWS(7, 64, g1, SF_INLINE);
-        else NFCS_ROWS(1, kBlock, g4, SF_INLINE);
+        NFCS_SHAPED(SF_INLINE);
     } else {
-        if (small) NFCS_ROWS(7, 64, g1, SF_DEFER);
-        else NFCS_ROWS(1, kBlock, g4, SF_DEFER);
-        if (small)
+        NFCS_SHAPED(SF_DEFER);
+        if (shape != kShapeLong)
             hipLaunchKernelGGL(apply_bytes_kernel<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
                                stream, arena, desc, n, base16, patch ? patch : ws);
         else
             hipLaunchKernelGGL(apply_bytes_kernel<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
                                stream, arena, desc, n, base16, patch ? patch : ws);
     }
+#undef NFCS_SHAPED
+#undef NFCS_ROWS8
 #undef NFCS_ROWS
     return hipGetLastError();
 }
@@ -1017,31 +1042,30 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
     if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
-    // Short frames (mean footprint under kSmallMeanBytes per packet) run in one-wave workgroups
-    // held at 7 waves/SIMD: short frames make short-lived waves, and single-wave workgroups retire
-    // and relaunch them with less granularity loss (C3 +2-3%); __launch_bounds__ 7 caps the kernel
-    // at 94 SGPRs (at the compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). The
-    // shape changes speed only: the store form is each wave's own (SF_DEFER).
-    // 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad bytes of (unused) LDS: at the
-    // 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768 vs 0.777, the 4M shard 0.710
-    // vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh); one-wave workgroups keep 8.
-    const bool small = arena_bytes / n < kSmallMeanBytes;
+    // The short shape's one-wave workgroups at 7 waves/SIMD: short frames make short-lived waves,
+    // and single-wave workgroups retire and relaunch them with less granularity loss (C3 +2-3%);
+    // __launch_bounds__ 7 caps the kernel at 94 SGPRs (at the compiler's 106 the SGPR file admits
+    // only 6 waves/SIMD: C3 +2%). 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad
+    // bytes of (unused) LDS: at the 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768
+    // vs 0.777, the 4M shard 0.710 vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh).
+    const uint64_t mean = arena_bytes / n;
+    const int shape = mean < kTinyMeanBytes ? kShapeTiny : (mean < kSmallMeanBytes ? kShapeShort : kShapeLong);
     // Long frames in a batch of more than kSubBatchAbovePackets: read pass and write pass alternate
     // per sub-batch of kSubBatchPackets, so the write pass finds its header lines still in the
     // 256 MB memory-side cache that the read pass just brought them into (the 4M
     // shard 0.683-0.714 -> 0.749-0.755). Sub-batches are multiples of 4 packets, so every wave's
     // deferral group is the same as in one launch; they run in order on the stream and share the
     // workspace.
-    if (form == kUpdateAuto && !small && n > kSubBatchAbovePackets) {
+    if (form == kUpdateAuto && shape == kShapeLong && n > kSubBatchAbovePackets) {
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(kSubBatchPackets, n - i),
                                                    base16, status ? status + i : nullptr,
-                                                   patch ? patch + i : nullptr, ws, form, small, stream);
+                                                   patch ? patch + i : nullptr, ws, form, shape, stream);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, small, stream);
+    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, shape, stream);
 }
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,

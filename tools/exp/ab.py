@@ -12,6 +12,8 @@ reference digest: parity is every variant's output digest equal to variant 0's o
 """
 import argparse
 import ctypes
+
+import numpy as np
 import json
 import os
 import sys
@@ -57,6 +59,10 @@ def main():
         if w.startswith("u"):
             uniform(eng, int(w[1:]), args, fn)
             continue
+        if w == "imix":  # simple IMIX: 64 / 570 / 1500-byte frames in the ratio 7:4:1
+            lens = np.random.default_rng(7).choice([64, 570, 1500], size=1 << 20, p=[7 / 12, 4 / 12, 1 / 12])
+            uniform(eng, lens, args, fn)
+            continue
         if w[0] == "c" and "n" in w[1:] and w[1:w.index("n", 1)].isdigit():  # c<k>n<N>: N packets of Ck
             cfg, n = int(w[1:w.index("n", 1)]), int(w[w.index("n", 1) + 1:])
         else:
@@ -101,24 +107,36 @@ def main():
 
 
 def uniform(eng, L, args, fn, n=1 << 20):
-    """1M IPv4+UDP frames of length L: random bytes, then the header fields of DESIGN.md §6."""
+    """1M IPv4+UDP frames of length L (an int, or one length per frame): random bytes, then the
+    header fields of DESIGN.md §6; 128-byte aligned slots."""
     import numpy as np
-    stride = (L + 127) // 128 * 128
-    rng = np.random.default_rng(L)
-    host = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
-    host[:, L:] = 0
-    host[:, 12], host[:, 13], host[:, 14], host[:, 15] = 0x08, 0x00, 0x45, 0x00
-    host[:, 16], host[:, 17] = (L - 14) >> 8, (L - 14) & 0xFF
-    host[:, 22], host[:, 23] = 64, 17
-    host[:, 24] |= 1
-    host[:, 38], host[:, 39] = (L - 34) >> 8, (L - 34) & 0xFF
+    lens = np.full(n, L, dtype=np.int64) if np.isscalar(L) else np.asarray(L, dtype=np.int64)
+    n = len(lens)
+    slots = (lens + 127) // 128 * 128
+    starts = np.concatenate([[0], np.cumsum(slots)[:-1]])
+    rng = np.random.default_rng(int(lens[0]) * 7 + n)
+    host = rng.integers(0, 256, size=int(slots.sum()), dtype=np.uint8)
+    tail = np.arange(int(slots.max()))
+    for Lv in np.unique(lens):  # zero each slot's bytes past its frame
+        idx = np.nonzero(lens == Lv)[0]
+        pad = tail[int(Lv):int((Lv + 127) // 128 * 128)]
+        if len(pad):
+            host[(starts[idx][:, None] + pad[None, :]).ravel()] = 0
+    def put(o, v):
+        host[starts + o] = v
+    put(12, 0x08); put(13, 0x00); put(14, 0x45); put(15, 0x00)
+    put(16, (lens - 14) >> 8); put(17, (lens - 14) & 0xFF)
+    put(22, 64); put(23, 17)
+    host[starts + 24] |= 1
+    put(38, (lens - 34) >> 8); put(39, (lens - 34) & 0xFF)
     desc = np.zeros(n, dtype=nf.DESC_DTYPE)
-    desc["off16"] = np.arange(n, dtype=np.uint32) * (stride // 16)
-    desc["len"] = L
+    desc["off16"] = (starts // 16).astype(np.uint32)
+    desc["len"] = lens.astype(np.uint32)
     arenas = [eng.alloc(host.nbytes).upload(host) for _ in range(args.fresh)]
     d_desc = eng.alloc(desc.nbytes).upload(desc)
     ws = eng.alloc(8 * n)
-    algo = float(L) * n + 12.0 * n
+    algo = float(lens.sum()) + 12.0 * n
+    L = "imix" if not np.isscalar(L) else L
     ms = ctypes.c_float()
     ref = None
     for v in [int(x) for x in args.variants.split(",")]:

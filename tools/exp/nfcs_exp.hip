@@ -23,6 +23,8 @@
 //               product itself uses 512K, kSubBatchPackets);  19  one launch pair, no sub-batches
 //       20/21   256K / 512K sub-batches with write pass i on a second stream, overlapping read pass i+1
 //       22/23   the product's launches (long-frame shape) with the write pass's stores plain / sc1
+//    24/25/26   8-lane rows (8 packets per wave) with 2 / 4 / 6 slots, inline, one-wave workgroups
+//       27/28   8-lane rows with 6 / 2 slots, per-group deferral + write pass
 // lds_pad: dynamic LDS bytes per workgroup, to cap the waves per SIMD (occupancy sweeps).
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
@@ -288,14 +290,15 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         const uint32_t S = variant == 16 ? (1u << 20) : (variant == 17 ? (1u << 19) : (1u << 21));
         for (uint32_t i = 0; i < n; i += S) {
             const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(S, n - i), 0u, nullptr,
-                                                   nullptr, ws, kUpdateAuto, arena_bytes / n < kSmallMeanBytes, st);
+                                                   nullptr, ws, kUpdateAuto, kShapeLong, st);
             if (e != hipSuccess) return e;
         }
         break;
     }
     case 19:  // the product form in ONE launch pair (no sub-batches), the round-2 session-1/2 form
         return launch_update_one(arena, arena_bytes, desc, n, 0u, nullptr, nullptr, ws, kUpdateAuto,
-                                 arena_bytes / n < kSmallMeanBytes, st);
+                                 arena_bytes / n < kTinyMeanBytes ? kShapeTiny
+                                 : (arena_bytes / n < kSmallMeanBytes ? kShapeShort : kShapeLong), st);
     case 20:
     case 21: {  // sub-batches of 256K (20) / 512K (21): read pass i+1 overlaps write pass i on a second stream
         static hipStream_t s2 = nullptr;
@@ -339,6 +342,34 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
                 hipLaunchKernelGGL(apply_pol_kernel<1>, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, st, arena,
                                    desc + i, m, ws);
         }
+        break;
+    }
+    case 24:  // 8-lane rows, 2 slots (256 B per row batch), 8 packets per wave, one-wave workgroups, inline
+        hipLaunchKernelGGL((update_rows_kernel<2, 8, 8, 64, false, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0u, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr,
+                           (nfcs_patch*)nullptr, nofwd);
+        break;
+    case 25:  // 8-lane rows, 4 slots (512 B per row batch)
+        hipLaunchKernelGGL((update_rows_kernel<4, 8, 8, 64, false, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0u, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr,
+                           (nfcs_patch*)nullptr, nofwd);
+        break;
+    case 26:  // 8-lane rows, 6 slots (768 B per row batch)
+        hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, false, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0u, st,
+                           arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr,
+                           (nfcs_patch*)nullptr, nofwd);
+        break;
+    case 27:
+    case 28: {  // 8-lane rows with 6 (27) / 2 (28) slots, SF_DEFER (per group of 4) + write pass
+        if (variant == 27)
+            hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, false, SF_DEFER>), dim3((n + 7u) / 8u), dim3(64), 0u,
+                               st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws,
+                               nofwd);
+        else
+            hipLaunchKernelGGL((update_rows_kernel<2, 8, 8, 64, false, SF_DEFER>), dim3((n + 7u) / 8u), dim3(64), 0u,
+                               st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws,
+                               nofwd);
+        hipLaunchKernelGGL(apply_bytes_kernel<false>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     }
     default: return hipErrorInvalidValue;
