@@ -1075,6 +1075,13 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     (void)di;
     if (n == 0) return hipSuccess;
     const FwdArgs fa = {nh, table, table_n};
+    if (arena_bytes / n < kTinyMeanBytes) {
+        // short frames: 8-lane rows, 8 packets per one-wave workgroup (packet-rate bound, §5g)
+        hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, true, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0,
+                           stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr,
+                           (nfcs_patch*)nullptr, fa);
+        return hipGetLastError();
+    }
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
     // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
     hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_INLINE>), dim3((n + 15u) / 16u),
