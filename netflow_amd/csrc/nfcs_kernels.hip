@@ -1135,33 +1135,33 @@ DEV uint32_t dpp_next(uint32_t x) {  // lane rl gets lane rl+1 of its row (0 for
 // Edited chunks of one batch. v: old chunks rl + 16k (+ cb); prevw: for a push, the old dword
 // just before this batch (the row's lane 15 of the previous batch); nextx: for a pop, the old
 // dword just after it. Batch 0 (first = true) builds the new bytes 12-15 in chunk 0.
-template <int K>
+template <int K, int R = 16>
 DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t rl, bool first,
                    uint32_t prevw, uint32_t nextx, uint32_t tag_dw, uint32_t cb, uint32_t wend) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint4 e = v[k];
         if (mode == VM_PUSH) {  // new[o] = old[o - 4] for o >= 16
-            uint32_t pw = dpp_prev(v[k].w);
-            const uint32_t lw = (k > 0) ? row_bcast<15, 16>(v[k - 1].w) : prevw;
+            uint32_t pw = dpp_prev(v[k].w);  // across an 8-lane row's start: replaced below
+            const uint32_t lw = (k > 0) ? row_bcast<R - 1, R>(v[k - 1].w) : prevw;
             if (rl == 0) pw = lw;
             e = make_uint4(pw, v[k].x, v[k].y, v[k].z);
             if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, tag_dw);
         } else if (mode == VM_POP) {  // new[o] = old[o + 4] for o >= 12
-            uint32_t nx = dpp_next(v[k].x);
-            const uint32_t fx = (k + 1 < K) ? row_bcast<0, 16>(v[k + 1 < K ? k + 1 : k].x) : nextx;
-            if (rl == 15) nx = fx;
+            uint32_t nx = dpp_next(v[k].x);  // across an 8-lane row's end: replaced below
+            const uint32_t fx = (k + 1 < K) ? row_bcast<0, R>(v[k + 1 < K ? k + 1 : k].x) : nextx;
+            if (rl == (uint32_t)R - 1u) nx = fx;
             e = make_uint4(v[k].y, v[k].z, v[k].w, nx);
             if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, nx);
         } else if (mode == VM_RETAG) {
             if (first && k == 0 && rl == 0) e.w = tag_dw;
         }
-        const uint32_t c = cb + rl + 16u * (uint32_t)k;
+        const uint32_t c = cb + rl + (uint32_t)R * (uint32_t)k;
         nv[k] = keep_tail(e, v[k], 16u * c, wend);
     }
 }
 
-template <int K, int K2 = 2, bool WT = false>
+template <int K, int K2 = 2, bool WT = false, int R = 16>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1170,15 +1170,15 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
                                                            const uint32_t* __restrict__ caps,
                                                            uint32_t cap_all,
                                                            uint8_t* __restrict__ status) {
-    constexpr int R = 16;
-    constexpr uint32_t PW = 4, KR = (uint32_t)(K * R);
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & 15u, row = lane >> 4;
-    const uint32_t rowbase4 = (lane & ~15u) * 4u;
+    static_assert(R == 16 || R == 8, "16- or 8-lane rows");
+    constexpr uint32_t PW = 64 / R, KR = (uint32_t)(K * R);
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
     const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
     const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
     uint32_t op = op_all, cap = cap_all;
-    {  // the wave's four edit words / capacities: scalar loads, like the descriptors
+    {  // the wave's edit words / capacities: scalar loads, like the descriptors
         uint32_t q[PW], r[PW];
 #pragma unroll
         for (uint32_t i = 0; i < PW; ++i) {
@@ -1229,8 +1229,8 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     const uint32_t nst = !act ? 0u : mode == VM_RETAG ? 1u : (wend + 15u) >> 4;  // chunks stored
 
     uint4 nv[K];
-    vlan_edit<K>(nv, v, mode, rl, true, 0u, nx0, tag_dw, 0u, wend);
-    uint32_t carry = row_bcast<15, 16>(v[K - 1].w);  // push: old dword before batch 1
+    vlan_edit<K, R>(nv, v, mode, rl, true, 0u, nx0, tag_dw, 0u, wend);
+    uint32_t carry = row_bcast<R - 1, R>(v[K - 1].w);  // push: old dword before batch 1
 
     // update_checksums() on the edited frame (690 / 718)
     RPlan P = fast_plan<R>(nv[0], rowbase4, nlen);
@@ -1293,8 +1293,8 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
                 w[k] = ld16<1>((c < nl) ? src + c : &g_zero16);
             }
             const uint32_t nx = *(const uint32_t*)((cb + KR2 < nl) ? src + cb + KR2 : &g_zero16);
-            vlan_edit<K2>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
-            carry = row_bcast<15, 16>(w[K2 - 1].w);
+            vlan_edit<K2, R>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
+            carry = row_bcast<R - 1, R>(w[K2 - 1].w);
 #pragma unroll
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
@@ -1363,13 +1363,17 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
                        uint32_t cap_all, uint8_t* status, hipStream_t stream) {
     (void)di;
     if (n == 0) return hipSuccess;
-    const uint32_t blocks = (n + 15u) / 16u;  // 4 rows per wave, 4 waves per workgroup
     // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD); batches of 2 slots
     // (94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, capping the occupancy lower
     // slower still (profiles/r01_s2_occupancy.md). Frame stores write-through (sc1): +1.2% on C1
     // push/pop over plain stores; dispatch order (the XCD-aware order measured 2% slower here).
-    hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3(blocks), dim3(kBlock), 0, stream, arena,
-                       arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    // Short frames (mean footprint < kTinyMeanBytes): 8-lane rows, 8 packets per wave (§5g).
+    if (arena_bytes / n < kTinyMeanBytes)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, 8>), dim3((n + 31u) / 32u), dim3(kBlock), 0, stream,
+                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    else  // 4 rows per wave, 4 waves per workgroup
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3((n + 15u) / 16u), dim3(kBlock), 0, stream,
+                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     return hipGetLastError();
 }
 
