@@ -372,6 +372,16 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL(apply_bytes_kernel<false>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
         break;
     }
+    case 29:
+    case 30: {  // the product form over consecutive sub-batches of 256K (29) / 128K (30) packets
+        const uint32_t S = variant == 29 ? (1u << 18) : (1u << 17);
+        for (uint32_t i = 0; i < n; i += S) {
+            const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(S, n - i), 0u, nullptr,
+                                                   nullptr, ws, kUpdateAuto, kShapeLong, st);
+            if (e != hipSuccess) return e;
+        }
+        break;
+    }
     default: return hipErrorInvalidValue;
     }
 #undef NFCS_X
