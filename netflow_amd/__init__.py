@@ -79,6 +79,7 @@ def _declare(L):
         "nfcs_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
         "nfcs_ctx_destroy": ([_vp], ctypes.c_int),
         "nfcs_ctx_stream": ([_vp], _vp),
+        "nfcs_ctx_set_slot_bytes": ([_vp, ctypes.c_uint32], ctypes.c_int),
         "nfcs_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
         "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
@@ -217,6 +218,11 @@ class Engine:
     @property
     def stream(self) -> int:
         return lib().nfcs_ctx_stream(self.ctx)
+
+    def set_slot_bytes(self, nbytes: int):
+        """Launch-shape hint for the device-path calls that follow (nfcs_ctx_set_slot_bytes): the
+        mean arena bytes per frame of bursts that fill only part of their arena; 0 = arena_bytes / n."""
+        _check(lib().nfcs_ctx_set_slot_bytes(self.ctx, int(nbytes)), "set_slot_bytes")
 
     def host_numa(self) -> tuple[int, bool]:
         """(NUMA node of this GPU or -1, whether the host staging ring is bound to it)."""

@@ -63,6 +63,7 @@ struct nfcs_ctx {
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
+    uint32_t slot_bytes = 0;  // launch-shape hint (nfcs_ctx_set_slot_bytes); 0 = arena_bytes / n
 };
 
 namespace {
@@ -308,7 +309,7 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
         if (e == hipSuccess)
             e = nfcs::launch_update(c->di, d_arena, arena_bytes, c->d_desc[s], m, 0u,
                                     h_status ? c->d_status[s] : nullptr, nullptr, nullptr,
-                                    nfcs::kUpdateInline, st);
+                                    nfcs::kUpdateInline, st, c->slot_bytes);
         if (e == hipSuccess && h_status)
             e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
@@ -332,7 +333,7 @@ int update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfc
                   uint32_t n, uint8_t* d_status, nfcs_patch* d_patch, hipStream_t st) {
     if (!d_patch) NFCS_HIP(acquire_ws(c, n, st));
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0u, d_status, d_patch,
-                                 d_patch ? nullptr : c->ws, nfcs::kUpdateAuto, st));
+                                 d_patch ? nullptr : c->ws, nfcs::kUpdateAuto, st, c->slot_bytes));
     if (!d_patch) NFCS_HIP(release_ws(c, st));
     return NFCS_OK;
 }
@@ -412,6 +413,12 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
 
 NFCS_API void* nfcs_ctx_stream(nfcs_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* c, uint32_t bytes) {
+    if (!c) return NFCS_EINVAL;
+    c->slot_bytes = bytes;
+    return NFCS_OK;
+}
+
 NFCS_API int nfcs_ctx_host_numa(nfcs_ctx* c, int* node, int* local) {
     if (!c || !node || !local) return NFCS_EINVAL;
     const int rc = ensure_host_pipeline(c);
@@ -443,7 +450,7 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
     if (!d_arena || !d_desc || !d_nh || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (table_n > 0 && (!d_table || ((uintptr_t)d_table & 3u))) return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
-                                     d_status, pick(c, stream)));
+                                     d_status, pick(c, stream), c->slot_bytes));
     return NFCS_OK;
 }
 
@@ -458,7 +465,7 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
-                               cap_all, d_status, pick(c, stream)));
+                               cap_all, d_status, pick(c, stream), c->slot_bytes));
     return NFCS_OK;
 }
 
@@ -771,7 +778,7 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
-                                         table_n, d_status, st));
+                                         table_n, d_status, st, c->slot_bytes));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -789,7 +796,8 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it)
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
-                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st));
+                                   (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
+                                   c->slot_bytes));
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

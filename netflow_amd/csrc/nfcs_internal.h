@@ -61,18 +61,25 @@ constexpr uint64_t kTinyMeanBytes = 800;
 // Dynamic LDS per 256-thread checksum workgroup (unused): 6 workgroups = 6 waves/SIMD per CU.
 constexpr unsigned kRowsLdsPad = 24576;
 
+// The mean arena bytes per packet that pick a launch shape (speed only): the context's slot-size
+// hint (nfcs_ctx_set_slot_bytes) when set, else arena_bytes / n.
+inline uint64_t shape_mean(uint64_t arena_bytes, uint32_t n, uint64_t slot_bytes) {
+    return slot_bytes ? slot_bytes : arena_bytes / n;
+}
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream);
+                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
+                         uint64_t slot_bytes = 0);
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream);
+                             hipStream_t stream, uint64_t slot_bytes = 0);
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream);
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes = 0);
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,

@@ -1037,7 +1037,8 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
-                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream) {
+                         nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
+                         uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
@@ -1048,7 +1049,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     // only 6 waves/SIMD: C3 +2%). 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad
     // bytes of (unused) LDS: at the 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768
     // vs 0.777, the 4M shard 0.710 vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh).
-    const uint64_t mean = arena_bytes / n;
+    const uint64_t mean = shape_mean(arena_bytes, n, slot_bytes);
     const int shape = mean < kTinyMeanBytes ? kShapeTiny : (mean < kSmallMeanBytes ? kShapeShort : kShapeLong);
     // Long frames in a batch of more than kSubBatchAbovePackets: read pass and write pass alternate
     // per sub-batch of kSubBatchPackets, so the write pass finds its header lines still in the
@@ -1071,11 +1072,11 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream) {
+                             hipStream_t stream, uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
     const FwdArgs fa = {nh, table, table_n};
-    if (arena_bytes / n < kTinyMeanBytes) {
+    if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes) {
         // short frames: 8-lane rows, 8 packets per one-wave workgroup (packet-rate bound, §5g)
         hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, true, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0,
                            stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr,
@@ -1360,7 +1361,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream) {
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
     // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD); batches of 2 slots
@@ -1368,7 +1369,7 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
     // slower still (profiles/r01_s2_occupancy.md). Frame stores write-through (sc1): +1.2% on C1
     // push/pop over plain stores; dispatch order (the XCD-aware order measured 2% slower here).
     // Short frames (mean footprint < kTinyMeanBytes): 8-lane rows, 8 packets per wave (§5g).
-    if (arena_bytes / n < kTinyMeanBytes)
+    if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, 8>), dim3((n + 31u) / 32u), dim3(kBlock), 0, stream,
                            arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
     else  // 4 rows per wave, 4 waves per workgroup

@@ -51,6 +51,7 @@ def test_error_conventions_without_gpu(lib):
     assert lib.nfcs_update_device(None, None, 0, None, 0, None, None, None) == -1
     assert lib.nfcs_update_host(None, None, 0, None, 0, None, 0) == -1
     assert lib.nfcs_ctx_create(0, None) == -1
+    assert lib.nfcs_ctx_set_slot_bytes(None, 128) == -1
     c = ctypes.c_void_p()
     rc = lib.nfcs_ctx_create(0, ctypes.byref(c))
     if not os.path.exists("/dev/kfd"):

@@ -1,0 +1,88 @@
+"""The launch-shape hint (nfcs_ctx_set_slot_bytes, include/nfcs.h): a burst that fills a small part
+of a large arena (a NIC ring) runs the shape its frames call for when the caller states their mean
+slot size. The hint picks speed only: every shape (8-lane rows, 16-lane one-wave workgroups,
+256-thread workgroups with deferred stores) must give the reference's bytes, statuses and lengths
+for the update, the fused L3 forward and VLAN push/pop, checked against the oracle."""
+import numpy as np
+import pytest
+
+import oracle
+from l3_common import random_l3_case
+from vlan_common import random_vlan_case
+
+pytestmark = pytest.mark.gpu
+HINTS = (0, 128, 1000, 4096)  # 0 = arena_bytes / n; then tiny / short / long shapes
+SLACK = 256 << 20  # arena bytes past the burst: with no hint the long shape runs
+
+
+@pytest.fixture
+def hinted(engine):
+    yield engine
+    engine.set_slot_bytes(0)  # the session engine goes back to arena_bytes / n
+
+
+def test_update_every_shape_matches_oracle(hinted):
+    frames = oracle.fuzz_frames(33, 0, 70000)  # above kInlineMaxPackets: deferral applies in the long shape
+    arena, desc = oracle.pack_frames(frames, align=128)
+    n = len(desc)
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    d_desc = hinted.alloc(desc.nbytes).upload(desc)
+    d_st = hinted.alloc(n)
+    d_arena = hinted.alloc(arena.nbytes + SLACK)
+    for hint in HINTS:
+        hinted.set_slot_bytes(hint)
+        d_arena.upload(arena)
+        hinted.update_device(d_arena, arena.nbytes + SLACK, d_desc, n, d_st)
+        hinted.sync()
+        assert np.array_equal(d_st.download(np.uint8, n), rst), hint
+        assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), hint
+    for b in (d_arena, d_desc, d_st):
+        b.free()
+
+
+def test_l3_forward_every_shape_matches_oracle(hinted):
+    frames, table, nh = random_l3_case(24, 30000, table_n=8)
+    arena, desc = oracle.pack_frames(frames)
+    n = len(desc)
+    ref = arena.copy()
+    rst = oracle.l3_forward_batch(ref, desc, nh, table)
+    table = np.ascontiguousarray(table, dtype=np.uint8).reshape(-1, 12)
+    d_desc = hinted.alloc(desc.nbytes).upload(desc)
+    d_nh = hinted.alloc(4 * n).upload(np.ascontiguousarray(nh, dtype=np.uint32))
+    d_tab = hinted.alloc(table.nbytes).upload(table)
+    d_st = hinted.alloc(n)
+    d_arena = hinted.alloc(arena.nbytes + SLACK)
+    for hint in HINTS:
+        hinted.set_slot_bytes(hint)
+        d_arena.upload(arena)
+        hinted.l3_forward_device(d_arena, arena.nbytes + SLACK, d_desc, d_nh, n, d_tab, len(table), d_st)
+        hinted.sync()
+        assert np.array_equal(d_st.download(np.uint8, n), rst), hint
+        assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), hint
+    for b in (d_arena, d_desc, d_nh, d_tab, d_st):
+        b.free()
+
+
+def test_vlan_every_shape_matches_oracle(hinted):
+    frames, ops, caps = random_vlan_case(44, 20000)
+    arena, desc = oracle.pack_frames(frames, room=4)
+    n = len(desc)
+    ref, rdesc = arena.copy(), desc.copy()
+    rst = oracle.vlan_batch(ref, rdesc, ops, caps)
+    d_desc = hinted.alloc(desc.nbytes)
+    d_ops = hinted.alloc(4 * n).upload(np.ascontiguousarray(ops, dtype=np.uint32))
+    d_caps = hinted.alloc(4 * n).upload(np.ascontiguousarray(caps, dtype=np.uint32))
+    d_st = hinted.alloc(n)
+    d_arena = hinted.alloc(arena.nbytes + SLACK)
+    for hint in HINTS:
+        hinted.set_slot_bytes(hint)
+        d_arena.upload(arena)
+        d_desc.upload(desc)
+        hinted.vlan_device(d_arena, arena.nbytes + SLACK, d_desc, n, d_ops, 0, d_caps, 0, d_st)
+        hinted.sync()
+        assert np.array_equal(d_st.download(np.uint8, n), rst), hint
+        assert np.array_equal(d_desc.download(np.dtype(desc.dtype), n), rdesc), hint
+        assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), hint
+    for b in (d_arena, d_desc, d_ops, d_caps, d_st):
+        b.free()

@@ -216,6 +216,45 @@ __global__ __launch_bounds__(kBlock) void apply_pol_kernel(uint8_t* __restrict__
     }
 }
 
+// Write-pass probes (variants 33/34). MODE 0: apply_bytes_kernel<true>'s loads and decision only, no
+// stores (the pass's launch + load round trip). MODE 1: 4 lanes per packet (lane j of the quad
+// loads the packet's descriptor and record itself and writes byte j): no cross-lane permutes,
+// 4x the threads.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void apply_probe_kernel(uint8_t* __restrict__ arena,
+                                                             const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                             const nfcs_patch* __restrict__ rec, uint32_t* sink) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (MODE == 0) {
+        const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
+        const uint2 r0 = i < n ? ((const uint2*)rec)[i] : make_uint2(0u, 0u);
+        uint32_t s = defer_len(d.len);
+        s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);
+        s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);
+        const bool dfr = i < n && defer_group(s, 4);
+        const uint32_t v = dfr ? (r0.x ^ r0.y ^ d.off16) : 0u;
+        if (v == 0x9E3779B9u && lane == 7u) sink[0] = v;  // never true on real records
+        return;
+    }
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t p = t >> 2;
+    const uint32_t j = lane & 3u;
+    const nfcs_desc d = p < n ? desc[p] : nfcs_desc{0u, 0u};
+    const uint2 r = p < n ? ((const uint2*)rec)[p] : make_uint2(0u, 0u);
+    const uint32_t s = row_sum<16>(j == 0 ? defer_len(d.len) : 0u);
+    if (!(p < n && defer_group(s, 4))) return;
+    const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
+    const uint32_t off = j < 2 ? ipo : l4o;
+    const uint32_t a = off + (j & 1u);
+    const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+    if (off != NFCS_PATCH_NONE && !overlap) {
+        const uint32_t b = (r.y >> (8u * j)) & 0xFFu;
+        uint8_t* q = arena + (uint64_t)d.off16 * 16u + a;
+        asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(q), "v"(b) : "memory");
+    }
+}
+
 static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc,
                              uint32_t n, nfcs_patch* ws, unsigned lds_pad, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0};
@@ -380,6 +419,25 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
                                                    nullptr, ws, kUpdateAuto, kShapeLong, st);
             if (e != hipSuccess) return e;
         }
+        break;
+    }
+    case 31:  // the write pass alone, over the records of the last call
+        hipLaunchKernelGGL(apply_bytes_kernel<true>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        break;
+    case 32:  // the long-shape read pass alone (records for deferred waves, no write pass)
+        hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_DEFER>), g4, dim3(kBlock), kRowsLdsPad,
+                           st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        break;
+    case 33:  // the write pass's loads and decision only
+        hipLaunchKernelGGL(apply_probe_kernel<0>, ga, dim3(kBlock), 0, st, arena, desc, n, ws, (uint32_t*)ws);
+        break;
+    case 34:  // the product read pass + the 4-lanes-per-packet write pass
+    case 35: {  // that write pass alone
+        if (variant == 34)
+            hipLaunchKernelGGL((update_rows_kernel<6, 16, 1, kBlock, false, SF_DEFER>), g4, dim3(kBlock), kRowsLdsPad,
+                               st, arena, arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        const dim3 gq((uint32_t)(((uint64_t)n * 4u + kBlock - 1) / kBlock));
+        hipLaunchKernelGGL(apply_probe_kernel<1>, gq, dim3(kBlock), 0, st, arena, desc, n, ws, (uint32_t*)ws);
         break;
     }
     default: return hipErrorInvalidValue;
