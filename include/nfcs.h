@@ -162,7 +162,10 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
  * by host threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs
  * per chunk, and only the 8-byte nfcs_patch records come back and are applied on the host.
  * flags:
- *   NFCS_HOST_FRAMES     copy whole frames back instead of patch records (same bytes, slower)
+ *   NFCS_HOST_FRAMES     copy whole frames back instead of patch records (same bytes, slower;
+ *                        each chunk's span goes back whole, so bytes between the burst's frames
+ *                        are rewritten with the values read: not for a ring whose other slots
+ *                        are being filled meanwhile — the default writes only checksum bytes)
  *   NFCS_HOST_ZERO_COPY  pinned arenas only: the kernel reads the frames over PCIe in place and
  *                        writes the checksum bytes straight back (no staging copies)
  *   NFCS_HOST_PATCH_ONLY the default since ABI 1 session 2; accepted and ignored
