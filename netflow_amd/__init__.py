@@ -164,19 +164,24 @@ class DeviceBuffer:
         _check(lib().nfcs_device_alloc(engine.ctx, max(self.nbytes, 16), ctypes.byref(p)), "device_alloc")
         self.ptr = p.value
 
-    def upload(self, a: np.ndarray):
+    def upload(self, a: np.ndarray, offset: int = 0):
+        """Copy `a` into the buffer at byte `offset`."""
         a = np.ascontiguousarray(a)
-        assert a.nbytes <= self.nbytes
+        if offset < 0 or offset + a.nbytes > self.nbytes:
+            raise NfcsError(f"upload of {a.nbytes} B at {offset} past a {self.nbytes}-byte buffer")
         if a.nbytes:
-            _check(lib().nfcs_memcpy_h2d(self.engine.ctx, self.ptr, a.ctypes.data, a.nbytes), "h2d")
+            _check(lib().nfcs_memcpy_h2d(self.engine.ctx, self.ptr + offset, a.ctypes.data, a.nbytes), "h2d")
         return self
 
-    def download(self, dtype=np.uint8, count: int | None = None) -> np.ndarray:
+    def download(self, dtype=np.uint8, count: int | None = None, offset: int = 0) -> np.ndarray:
+        """`count` items of `dtype` from byte `offset` (default: the rest of the buffer)."""
         dtype = np.dtype(dtype)
-        count = self.nbytes // dtype.itemsize if count is None else count
+        count = (self.nbytes - offset) // dtype.itemsize if count is None else count
+        if offset < 0 or offset + count * dtype.itemsize > self.nbytes:
+            raise NfcsError(f"download of {count} x {dtype} at {offset} past a {self.nbytes}-byte buffer")
         out = np.empty(count, dtype=dtype)
         if out.nbytes:
-            _check(lib().nfcs_memcpy_d2h(self.engine.ctx, out.ctypes.data, self.ptr, out.nbytes), "d2h")
+            _check(lib().nfcs_memcpy_d2h(self.engine.ctx, out.ctypes.data, self.ptr + offset, out.nbytes), "d2h")
         return out
 
     def free(self):

@@ -1,0 +1,116 @@
+"""Maximum-size addressing: a descriptor's off16 is a u32 count of 16-byte units, so an arena can
+reach 64 GiB and a frame's byte offset needs 36 bits. Frames placed past 32 GiB (off16 >= 2^31: a
+signed 32-bit offset would go negative, a 32-bit byte offset would wrap) through every device entry
+point — the checksum update (inline and deferred stores), the fused L3 forward, VLAN push/pop,
+flow keys and the digest — must give the oracle's bytes, byte for byte, and leave the arena
+around them untouched. The region's own offsets are shifted by the base for the device."""
+import numpy as np
+import pytest
+
+import netflow_amd as nf
+import oracle
+from l3_common import random_l3_case
+from vlan_common import random_vlan_case
+
+pytestmark = pytest.mark.gpu
+BASE = (32 << 30) + 4096  # byte offset of the region: off16 = 2^31 + 256
+GUARD = 1 << 20           # arena bytes after the region (checked untouched)
+
+
+@pytest.fixture(scope="module")
+def big(engine):
+    b = engine.alloc(BASE + (96 << 20) + GUARD)
+    yield b
+    b.free()
+
+
+def place(engine, big, arena, desc):
+    """Upload the region at BASE with a guard pattern after it; device descriptors shifted."""
+    big.upload(arena, BASE)
+    big.upload(np.full(GUARD, 0xA5, np.uint8), BASE + arena.nbytes)
+    d = desc.copy()
+    d["off16"] = d["off16"].astype(np.uint64) + BASE // 16
+    assert int(d["off16"].min()) >= 1 << 31
+    return engine.alloc(max(d.nbytes, 16)).upload(d), BASE + arena.nbytes + GUARD
+
+
+def region(big, nbytes):
+    out = big.download(np.uint8, nbytes + GUARD, BASE)
+    assert (out[nbytes:] == 0xA5).all()  # nothing written past the region
+    return out[:nbytes]
+
+
+def test_update_past_32_gib(engine, big):
+    frames = oracle.fuzz_frames(51, 0, 70000)  # > kInlineMaxPackets: inline and deferred waves
+    arena, desc = oracle.pack_frames(frames, align=128)
+    n = len(desc)
+    assert arena.nbytes + GUARD <= (96 << 20) + GUARD
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    d_desc, nbytes = place(engine, big, arena, desc)
+    d_st = engine.alloc(n)
+    assert engine.digest_device(big, nbytes, d_desc, n) == oracle.digest(arena, desc)
+    engine.update_device(big, nbytes, d_desc, n, d_st)
+    engine.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    assert np.array_equal(region(big, arena.nbytes), ref)
+    assert engine.digest_device(big, nbytes, d_desc, n) == oracle.digest(ref, desc)
+    d_desc.free()
+    d_st.free()
+
+
+def test_l3_forward_past_32_gib(engine, big):
+    frames, table, nh = random_l3_case(52, 20000, table_n=8)
+    arena, desc = oracle.pack_frames(frames)
+    n = len(desc)
+    ref = arena.copy()
+    rst = oracle.l3_forward_batch(ref, desc, nh, table)
+    table = np.ascontiguousarray(table, dtype=np.uint8).reshape(-1, 12)
+    d_desc, nbytes = place(engine, big, arena, desc)
+    d_nh = engine.alloc(4 * n).upload(np.ascontiguousarray(nh, dtype=np.uint32))
+    d_tab = engine.alloc(table.nbytes).upload(table)
+    d_st = engine.alloc(n)
+    engine.l3_forward_device(big, nbytes, d_desc, d_nh, n, d_tab, len(table), d_st)
+    engine.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    assert np.array_equal(region(big, arena.nbytes), ref)
+    for b in (d_desc, d_nh, d_tab, d_st):
+        b.free()
+
+
+def test_vlan_past_32_gib(engine, big):
+    frames, ops, caps = random_vlan_case(53, 20000)
+    arena, desc = oracle.pack_frames(frames, room=4)
+    n = len(desc)
+    ref, rdesc = arena.copy(), desc.copy()
+    rst = oracle.vlan_batch(ref, rdesc, ops, caps)
+    d_desc, nbytes = place(engine, big, arena, desc)
+    d_ops = engine.alloc(4 * n).upload(np.ascontiguousarray(ops, dtype=np.uint32))
+    d_caps = engine.alloc(4 * n).upload(np.ascontiguousarray(caps, dtype=np.uint32))
+    d_st = engine.alloc(n)
+    engine.vlan_device(big, nbytes, d_desc, n, d_ops, 0, d_caps, 0, d_st)
+    engine.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    got = d_desc.download(nf.DESC_DTYPE, n)
+    assert np.array_equal(got["len"], rdesc["len"])
+    assert np.array_equal(got["off16"].astype(np.uint64) - BASE // 16, rdesc["off16"].astype(np.uint64))
+    assert np.array_equal(region(big, arena.nbytes), ref)
+    for b in (d_desc, d_ops, d_caps, d_st):
+        b.free()
+
+
+def test_flow_keys_past_32_gib(engine, big):
+    frames = oracle.fuzz_frames(54, 0, 20000)
+    arena, desc = oracle.pack_frames(frames)
+    n = len(desc)
+    rrecs, rh = oracle.flow_keys_batch(arena, desc)
+    d_desc, nbytes = place(engine, big, arena, desc)
+    d_keys = engine.alloc(64 * n)
+    d_hash = engine.alloc(4 * n)
+    engine.flow_keys_device(big, nbytes, d_desc, n, d_keys, d_hash)
+    engine.sync()
+    assert np.array_equal(d_keys.download(np.uint8, 64 * n).reshape(n, 64), rrecs)
+    assert np.array_equal(d_hash.download(np.uint32, n), rh)
+    assert np.array_equal(region(big, arena.nbytes), arena)  # read only
+    for b in (d_desc, d_keys, d_hash):
+        b.free()
