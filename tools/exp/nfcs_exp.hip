@@ -440,6 +440,27 @@ static hipError_t exp_launch(int variant, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL(apply_probe_kernel<1>, gq, dim3(kBlock), 0, st, arena, desc, n, ws, (uint32_t*)ws);
         break;
     }
+    case 36:
+    case 37:
+    case 38:
+    case 39: {  // 8-lane rows with more slots (8 packets per wave, one-wave workgroups), SF_DEFER + write pass:
+        //        12 slots (1536 B per row pass) at 5 (36) / 4 (37) waves/SIMD, 8 slots (38, 6 waves), 10 (39, 5)
+        const dim3 g8((n + 7u) / 8u);
+        if (variant == 36)
+            hipLaunchKernelGGL((update_rows_kernel<12, 8, 5, 64, false, SF_DEFER>), g8, dim3(64), 0u, st, arena,
+                               arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        else if (variant == 37)
+            hipLaunchKernelGGL((update_rows_kernel<12, 8, 4, 64, false, SF_DEFER>), g8, dim3(64), 0u, st, arena,
+                               arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        else if (variant == 38)
+            hipLaunchKernelGGL((update_rows_kernel<8, 8, 6, 64, false, SF_DEFER>), g8, dim3(64), 0u, st, arena,
+                               arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        else
+            hipLaunchKernelGGL((update_rows_kernel<10, 8, 5, 64, false, SF_DEFER>), g8, dim3(64), 0u, st, arena,
+                               arena_bytes, desc, n, 0u, (uint8_t*)nullptr, (nfcs_patch*)nullptr, ws, nofwd);
+        hipLaunchKernelGGL(apply_bytes_kernel<false>, ga, dim3(kBlock), 0, st, arena, desc, n, 0u, ws);
+        break;
+    }
     default: return hipErrorInvalidValue;
     }
 #undef NFCS_X
