@@ -554,6 +554,12 @@ def main():
                      "traffic_read_write": None if traffic is None else
                      [int(traffic["fetch_bytes"]), int(traffic["write_bytes"])],
                      "kernel_ms": round(ev_ms, 4),
+                     "kernel_ms_spans": ("one nfcs_l3_forward_device call: update_rows_kernel<..., true, 0>" if l3 else
+                                         "one nfcs_vlan_device call: vlan_rows_kernel" if args.op == "vlan" else
+                                         "one nfcs_flow_keys_device call: flow_keys_kernel" if fk else
+                                         "one nfcs_update_device call: update_rows_kernel (read pass) + "
+                                         "apply_bytes_kernel (write pass) of every sub-batch; rocprofv3 lists "
+                                         "both, their averages add up to it"),
                      "algorithmic_bytes_per_launch": int(algo_bytes), **extra_roofline},
         "parity": parity,
     }
