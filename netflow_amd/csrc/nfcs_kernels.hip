@@ -503,6 +503,10 @@ DEV void st8(uint8_t* p, uint32_t b) {
     if (WT) __hip_atomic_store(p, (uint8_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = (uint8_t)b;
 }
+// A byte store that goes to memory past the caches (`sc0 sc1 nt`: system scope, non-temporal).
+DEV void st8_nt(uint8_t* p, uint32_t b) {
+    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");
+}
 template <bool WT>
 DEV void st16(uint4* p, const uint4& v) {
     if (WT) {
@@ -623,7 +627,7 @@ enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
 DEV bool defer_group(uint32_t lensum, uint32_t P) { return lensum >= P * (uint32_t)kDeferMeanBytes; }
 DEV uint32_t defer_len(uint32_t len) { return len < 0xFFFFu ? len : 0xFFFFu; }
 
-template <int K, int R = 16, bool FWD = false>
+template <int K, int R = 16, bool FWD = false, bool NT = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
                      const uint32_t* wmac = nullptr) {
@@ -749,12 +753,18 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     // The (at most 4) checksum bytes from lanes 0..3 of the row, write-through (sc1: the L2
     // keeps no dirty copy of the header line; session 3, C1 +2.5% / C3 +5% over write-back
     // stores; byte stores measured fastest against chunk, dword, whole-line and re-load-then-
-    // store forms), then the status byte / patch record from lane 0.
+    // store forms) or, with NT (the short-frame shape), past the caches (`sc0 sc1 nt`: round 2
+    // session 3, C3 +2%, uniform 1024-byte frames +2.7%; in the long shape it cost 64K-packet
+    // bursts of 9000-byte frames 3%, in 8-lane rows IMIX ±1%), then the status byte / patch
+    // record from lane 0.
     auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool stores) {
         if (stores && on && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w_ : ipw_;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<true>(frame + pos, w >> (16 + 8 * (rl & 1u)));
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) {
+                if (NT) st8_nt(frame + pos, w >> (16 + 8 * (rl & 1u)));
+                else st8<true>(frame + pos, w >> (16 + 8 * (rl & 1u)));
+            }
         }
         if (on && rl == 0) {
             if (status) status[S.p] = (uint8_t)st_;
@@ -924,7 +934,10 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
     RowStage<K> S;
     row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, nh);
-    row_process<K, R, FWD>(S, rl, rowbase4, status, rec, frame_stores, fa.table_n, wmac);
+    // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
+    // workgroups), write-through elsewhere (see row_process)
+    row_process<K, R, FWD, !FWD && R == 16 && BS == 64>(S, rl, rowbase4, status, rec, frame_stores,
+                                                         fa.table_n, wmac);
 }
 
 // SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
