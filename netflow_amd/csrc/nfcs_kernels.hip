@@ -507,6 +507,11 @@ DEV void st8(uint8_t* p, uint32_t b) {
 DEV void st8_nt(uint8_t* p, uint32_t b) {
     asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");
 }
+// The same for 16 bytes (the s_nop: see st16 below).
+DEV void st16_nt(uint4* p, const uint4& v) {
+    const u32x4_t t = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
+}
 template <bool WT>
 DEV void st16(uint4* p, const uint4& v) {
     if (WT) {
@@ -1175,7 +1180,21 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
     }
 }
 
-template <int K, int K2 = 2, bool WT = false, int R = 16>
+// Store policy of the VLAN kernel's frame writes: every write of a frame (its rewritten chunks and,
+// after them, its checksum bytes) takes the same path, so same-address writes stay in program order.
+enum : int { VST_PLAIN = 0, VST_WT = 1, VST_NT = 2 };
+template <int POL>
+DEV void vst16(uint4* p, const uint4& v) {
+    if (POL == VST_NT) st16_nt(p, v);
+    else st16<POL == VST_WT>(p, v);
+}
+template <int POL>
+DEV void vst8(uint8_t* p, uint32_t b) {
+    if (POL == VST_NT) st8_nt(p, b);
+    else st8<POL == VST_WT>(p, b);
+}
+
+template <int K, int K2 = 2, int POL = VST_PLAIN, int R = 16>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1287,13 +1306,13 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst || (k == 0 && patched)) st16<WT>((uint4*)frame + c, nv[k]);
+            if (c < nst || (k == 0 && patched)) vst16<POL>((uint4*)frame + c, nv[k]);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst) st16<WT>((uint4*)frame + c, nv[k]);
+            if (c < nst) vst16<POL>((uint4*)frame + c, nv[k]);
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
         // the rest of a long frame in batches of K2 slots (K2 < K saves VGPRs: w and e live
@@ -1313,7 +1332,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
-                if (c < nst) st16<WT>((uint4*)frame + c, e[k]);
+                if (c < nst) vst16<POL>((uint4*)frame + c, e[k]);
             }
         }
         l4w = finish(acc);
@@ -1323,7 +1342,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             const uint32_t w = (t < 2) ? ipw : l4w;
             const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
             if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl)
-                st8<WT>(frame + pos, w >> (16 + 8 * (t & 1u)));
+                vst8<POL>(frame + pos, w >> (16 + 8 * (t & 1u)));
         }
     }
     const uint32_t st0 = bad ? (uint32_t)NFCS_ST_BAD_DESC
@@ -1365,7 +1384,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
         if (slow && !seq && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w2 : ipw2;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) st8<WT>(frame + pos, w >> (16 + 8 * (rl & 1u)));
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE) vst8<POL>(frame + pos, w >> (16 + 8 * (rl & 1u)));
         }
         if (slow && rl == 0 && status)
             status[p] = (uint8_t)((seq ? (ost | NFCS_ST_FLAG_OVERLAP) : Q.st) | NFCS_ST_FLAG_VLAN);
@@ -1377,17 +1396,24 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
                        uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
-    // Long frames continue in batches of 6 slots (136 VGPRs, 3 waves/SIMD); batches of 2 slots
+    // Long frames continue in batches of 6 slots (128 VGPRs, 4 waves/SIMD); batches of 2 slots
     // (94 VGPRs, 5 waves/SIMD) measured 6% slower on C1 push/pop, capping the occupancy lower
-    // slower still (profiles/r01_s2_occupancy.md). Frame stores write-through (sc1): +1.2% on C1
-    // push/pop over plain stores; dispatch order (the XCD-aware order measured 2% slower here).
+    // slower still (profiles/r01_s2_occupancy.md); dispatch order (the XCD-aware order measured 2%
+    // slower here). Frame stores past the caches (`sc0 sc1 nt`, round 2 session 3): C1 push/pop
+    // +4.5%, 1M 256 / 512-byte frames +2-5% against write-through `sc1` (itself +1.2% over plain
+    // stores); frames in slots under 256 B keep `sc1` (64-byte frames: 177 vs 181 µs per 1M).
     // Short frames (mean footprint < kTinyMeanBytes): 8-lane rows, 8 packets per wave (§5g).
-    if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes)
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true, 8>), dim3((n + 31u) / 32u), dim3(kBlock), 0, stream,
-                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+    const uint64_t mean = shape_mean(arena_bytes, n, slot_bytes);
+    const dim3 g8((n + 31u) / 32u), g16((n + 15u) / 16u);
+    if (mean < kVlanWtMeanBytes)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_WT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
+                           desc, n, ops, op_all, caps, cap_all, status);
+    else if (mean < kTinyMeanBytes)
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
+                           desc, n, ops, op_all, caps, cap_all, status);
     else  // 4 rows per wave, 4 waves per workgroup
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, true>), dim3((n + 15u) / 16u), dim3(kBlock), 0, stream,
-                           arena, arena_bytes, desc, n, ops, op_all, caps, cap_all, status);
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT>), g16, dim3(kBlock), 0, stream, arena, arena_bytes,
+                           desc, n, ops, op_all, caps, cap_all, status);
     return hipGetLastError();
 }
 

@@ -11,7 +11,7 @@ from l3_common import random_l3_case
 from vlan_common import random_vlan_case
 
 pytestmark = pytest.mark.gpu
-HINTS = (0, 128, 1000, 4096)  # 0 = arena_bytes / n; then tiny / short / long shapes
+HINTS = (0, 128, 512, 1000, 4096)  # 0 = arena_bytes / n; then tiny (VLAN: sc1, nt) / short / long shapes
 SLACK = 256 << 20  # arena bytes past the burst: with no hint the long shape runs
 
 
