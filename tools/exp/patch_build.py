@@ -1,0 +1,36 @@
+"""patch_build.py — measurement tool (not product): builds libnfcs.so from the product sources with
+literal text substitutions in nfcs_kernels.hip (each OLD must occur exactly COUNT times, default 1),
+so a one-line policy or shape change can be A/B-timed against the product without touching it:
+  python tools/exp/patch_build.py OUT.so 'OLD' 'NEW' ['OLD' 'NEW' ...]
+  NFCS_LIB=OUT.so python bench.py --op flowkey --no-cpu
+Prefix OLD with '<N>*' to require N occurrences (all replaced)."""
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    out, pairs = sys.argv[1], sys.argv[2:]
+    if not pairs or len(pairs) % 2:
+        raise SystemExit(__doc__)
+    src = open(os.path.join(ROOT, "netflow_amd", "csrc", "nfcs_kernels.hip")).read()
+    for old, new in zip(pairs[::2], pairs[1::2]):
+        cnt = 1
+        if "*" in old[:4] and old.split("*", 1)[0].isdigit():
+            cnt, old = int(old.split("*", 1)[0]), old.split("*", 1)[1]
+        if src.count(old) != cnt:
+            raise SystemExit(f"{old!r}: {src.count(old)} occurrences, expected {cnt}")
+        src = src.replace(old, new)
+    with tempfile.TemporaryDirectory() as tmp:
+        k = os.path.join(tmp, "nfcs_kernels.hip")
+        open(k, "w").write(src)
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+                        "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "netflow_amd", "csrc"),
+                        k, os.path.join(ROOT, "netflow_amd", "csrc", "nfcs_api.hip"), "-o", out], check=True)
+
+
+if __name__ == "__main__":
+    main()
