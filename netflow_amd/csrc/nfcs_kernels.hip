@@ -616,8 +616,9 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 }
 
 // How update_rows_kernel's checksum bytes reach the frames:
-//   SF_INLINE   the row's lanes 0-3 store the 2+2 bytes write-through (sc1) as soon as they are
-//               known: one 64-byte write request per packet inside the read stream;
+//   SF_INLINE   the row's lanes 0-3 store the 2+2 bytes as soon as they are known, write-through
+//               (sc1) or, in the short-frame shape, past the caches (sc0 sc1 nt): one 64-byte
+//               write request per packet inside the read stream;
 //   SF_DEFER    per wave, from its four descriptor lengths (SGPRs): a wave whose frames average
 //               at least kDeferMeanBytes writes 8-byte patch records instead, and
 //               apply_bytes_kernel writes them after the read pass with non-temporal stores (the
