@@ -97,3 +97,61 @@ def test_l3_config_batch_vs_oracle(engine):
     assert np.array_equal(d_arena.download(np.uint8, nbytes), arena[:nbytes])
     assert ((rst & 0x80) != 0).sum() == (nh < 16).sum()  # TTL 64 everywhere: all routed ones go
     assert (rst[nh == 16] == nf.ST_NO_ROUTE).all()
+
+
+def _pad_groups(frames, rng, keep_every=5):
+    """Long-frame groups for the deferred forward: in every aligned group of 4 frames except one
+    in `keep_every`, each frame is extended to 1300-1500 bytes with random payload (its headers,
+    and so its parse and bounds checks, stay those of the fuzz frame), so those groups average
+    >= 1280 B and their waves defer; the kept groups store inline in the same launch."""
+    out = []
+    for i, f in enumerate(frames):
+        if (i // 4) % keep_every != 0 and len(f) < 1300:
+            f = f + rng.integers(0, 256, size=int(rng.integers(1300, 1501)) - len(f), dtype=np.uint8).tobytes()
+        out.append(f)
+    return out
+
+
+@pytest.mark.parametrize("align", [16, 128])
+def test_l3_deferred_fuzz_vs_oracle(engine, align):
+    """A burst above kInlineMaxPackets of mostly long frames: the read pass writes 16-byte forward
+    records for its deferring waves and apply_fwd_kernel stores TTL, checksums and MACs; every
+    header kind of the fuzz (tagged, options, IHL < 5, IPv6, ICMP, expired TTLs, no route) runs
+    through both store forms. Bytes and statuses against the oracle."""
+    n = 100_003  # ragged: the last group of 4 is partial
+    rng = np.random.default_rng(align + 7)
+    frames, table, nh = random_l3_case(31 + align, n, table_n=8)
+    frames = _pad_groups(frames, rng)
+    arena, desc = oracle.pack_frames(frames, align=align)
+    ref = arena.copy()
+    rst = oracle.l3_forward_batch(ref, desc, nh, table)
+    out, st = run_l3(engine, arena, desc, nh, table)
+    assert np.array_equal(st, rst)
+    assert np.array_equal(out, ref)
+    assert ((rst & 0x80) != 0).sum() > n // 4  # about a third of the fuzz frames forward
+
+
+def test_l3_deferred_sub_batches_vs_oracle(engine):
+    """Above kSubBatchAbovePackets the deferred forward runs as 512K-packet sub-batches (read pass,
+    write pass, next): 1.2M C1 frames with expired TTLs, missing routes and a ragged tail, against
+    the oracle byte for byte, statuses at each packet's own index."""
+    n = 1_200_003
+    arena, desc = oracle.gen_config(1, 20250620, 0, n, 128)
+    idx = np.arange(n)
+    ttl_at = desc["off16"].astype(np.int64) * 16 + 22
+    arena[ttl_at[idx % 7 == 3]] = 1  # TTL 1: expired, untouched
+    rng = np.random.default_rng(12)
+    table = rng.integers(0, 256, size=(8, 12), dtype=np.uint8)
+    nh = (idx % 9).astype(np.uint32)  # 8 = no route
+    d_arena = engine.alloc(arena.nbytes).upload(arena)
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_nh = engine.alloc(4 * n).upload(nh)
+    d_tab = engine.alloc(table.nbytes).upload(table)
+    d_st = engine.alloc(n)
+    rst = oracle.l3_forward_batch(arena, desc, nh, table)
+    engine.l3_forward_device(d_arena, arena.nbytes, d_desc, d_nh, n, d_tab, 8, d_st)
+    engine.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), arena)
+    assert (rst[idx % 7 == 3] == nf.ST_TTL_EXPIRED).all()
+    assert (rst[(idx % 9 == 8) & (idx % 7 != 3)] == nf.ST_NO_ROUTE).all()
