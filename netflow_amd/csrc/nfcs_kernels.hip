@@ -628,14 +628,6 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //               PCIe back).
 enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
 
-// The fused L3 forward's deferred record (SF_DEFER with FWD), 16 bytes per packet in the workspace:
-//   x  the header dword holding the decremented TTL (dword ipd - 1)
-//   y  the dword holding the IPv4 header checksum (dword ipd = (l2 + 10) / 4: 6, or 7 tagged)
-//   z  the dword holding the L4 checksum (dword l4d), the other bytes as read
-//   w  kFwdRecOn | ipd | l4d << 4 (l4d = 15: no L4 checksum), or 0: nothing to store
-// The MACs (dwords 0-2) come from the next-hop table in the write pass.
-constexpr uint32_t kFwdRecOn = 0x80000000u;
-
 // SF_DEFER's decision for the P packets pw .. pw+P-1 (lengths 0 past n), shared by the read pass
 // and apply_bytes_kernel so both pick the same waves.
 DEV bool defer_group(uint32_t lensum, uint32_t P) { return lensum >= P * (uint32_t)kDeferMeanBytes; }
@@ -764,9 +756,6 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         if ((P.flags & F_UDP) && c == 0) c = 0xFFFFu;  // 867-871
         l4w = P.fs | (c << 16);
     }
-    // the fused forward keeps its own 16-byte records (fwd_rec); the 8-byte patch records are the
-    // plain update's
-    nfcs_patch* const prec = FWD ? nullptr : rec;
     // The (at most 4) checksum bytes from lanes 0..3 of the row, write-through (sc1: the L2
     // keeps no dirty copy of the header line; session 3, C1 +2.5% / C3 +5% over write-back
     // stores; byte stores measured fastest against chunk, dword, whole-line and re-load-then-
@@ -785,11 +774,11 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         }
         if (on && rl == 0) {
             if (status) status[S.p] = (uint8_t)st_;
-            if (prec) {
+            if (rec) {
                 uint2 r;
                 r.x = (ipw_ & 0xFFFFu) | (l4w_ << 16);
                 r.y = (ipw_ >> 16) | (l4w_ & 0xFFFF0000u);
-                ((uint2*)prec)[S.p] = r;
+                ((uint2*)rec)[S.p] = r;
             }
         }
     };
@@ -800,18 +789,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         // patched in; unchanged bytes are rewritten with the values just read from them (a frame
         // never shares a 16-byte chunk with another frame). +1.5% over a 16-byte store + byte
         // stores (session 3).
-        // A deferred wave (SF_DEFER, !frame_stores) instead writes the header dwords the forward
-        // changes besides the MACs — TTL, IPv4 checksum, L4 checksum, each with the bytes around
-        // it as just read — into the packet's 16-byte fwd_rec, and apply_fwd_kernel stores them
-        // and the MACs after the read pass. Every IHL-5 header qualifies (the TTL and IPv4
-        // checksum dwords sit in chunk 1, the L4 checksum inside one dword of the first 64 bytes);
-        // a row that does not keeps its segment store.
-        const bool dfr = !frame_stores;
-        const uint32_t ipo = ipw & 0xFFFFu, l4o = l4w & 0xFFFFu;
-        const bool recok = dfr && (ipo == 24u || ipo == 28u) &&
-                           (l4o == NFCS_PATCH_NONE || (l4o < 62u && (l4o & 3u) != 3u));
-        const bool fw = S.valid && !slow && fwd;
-        if (fw) {
+        if (S.valid && !slow && fwd) {
             uint4 v = h0;
             uint32_t last = 1u;
 #pragma unroll
@@ -823,17 +801,8 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                     if ((pos >> 4) == rl) v = put_byte(v, pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
                 }
             }
-            if (recok) {
-                uint8_t* r = (uint8_t*)rec + 16ull * S.p;
-                if (rl == 1) *(uint2*)r = make_uint2(comp(v, (ipo >> 2) - 5u), comp(v, (ipo >> 2) - 4u));
-                if (l4o != NFCS_PATCH_NONE && rl == (l4o >> 4)) *(uint32_t*)(r + 8) = comp(v, (l4o >> 2) & 3u);
-            } else if (rl <= last && 16u * rl < len) {
-                st16<true>((uint4*)frame + rl, v);
-            }
+            if (rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
         }
-        if (dfr && S.valid && rl == 0)  // every packet of a deferred wave states whether it has a record
-            *(uint32_t*)((uint8_t*)rec + 16ull * S.p + 12u) =
-                (fw && recok) ? (kFwdRecOn | (ipo >> 2) | ((l4o == NFCS_PATCH_NONE ? 15u : (l4o >> 2)) << 4)) : 0u;
         emit(S.valid && !slow, st, ipw, l4w, false);
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
@@ -1032,45 +1001,6 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
     }
 }
 
-// The fused L3 forward's write pass (SF_DEFER): 8 lanes per packet, 8 packets per wave. Lane j of
-// a packet whose record is on stores one header dword — j = 0-2 the MACs of its next hop, 3 the
-// TTL dword, 4 the IPv4 checksum dword, 5 the L4 checksum dword — so the packet's 24 bytes, all in
-// its first 64 bytes, leave in ONE store instruction as one write request with a byte mask,
-// non-temporal at system scope as in apply_bytes_kernel. The deferral decision of each aligned
-// group of 4 packets is recomputed from their lengths (0 past n), as the read pass made it, so
-// records of waves that stored inline (stale) are never read.
-__global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__ arena,
-                                                           const nfcs_desc* __restrict__ desc,
-                                                           uint32_t n, const uint32_t* __restrict__ nh,
-                                                           const nfcs_nexthop* __restrict__ table,
-                                                           const uint4* __restrict__ rec) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t p = t >> 3, g = p & ~3ull;
-    const uint32_t j = (uint32_t)t & 7u;
-    if (p >= n) return;
-    uint32_t s = 0, off16 = 0;
-    if (g + 4 <= n) {
-        const uint4 a = ((const uint4*)(desc + g))[0], b = ((const uint4*)(desc + g))[1];
-        s = defer_len(a.y) + defer_len(a.w) + defer_len(b.y) + defer_len(b.w);
-        const uint32_t k = (uint32_t)(p - g);
-        off16 = k == 0 ? a.x : (k == 1 ? a.z : (k == 2 ? b.x : b.z));
-    } else {
-        for (uint64_t i = g; i < n; ++i) s += defer_len(desc[i].len);
-        off16 = desc[p].off16;
-    }
-    if (!defer_group(s, 4) || j >= 6) return;
-    const uint4 r = rec[p];
-    if (!(r.w & kFwdRecOn)) return;
-    const uint32_t ipd = r.w & 15u, l4d = (r.w >> 4) & 15u;
-    if (j == 5 && l4d == 15u) return;
-    const uint32_t* m = (const uint32_t*)(table + nh[p]);
-    const uint32_t idx = j < 3 ? j : (j == 3 ? ipd - 1u : (j == 4 ? ipd : l4d));
-    const uint32_t mj = m[j < 3 ? j : 0];
-    const uint32_t val = j < 3 ? mj : (j == 3 ? r.x : (j == 4 ? r.y : r.z));
-    uint32_t* a = (uint32_t*)(arena + (uint64_t)off16 * 16u) + idx;
-    asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(a), "v"(val) : "memory");
-}
-
 // Workgroup shapes of the checksum read pass, chosen per call from the mean arena footprint per
 // packet (speed only: results and store forms never depend on it):
 //   kShapeTiny   (< kTinyMeanBytes)  8-lane rows of 6 slots (768 B per row pass), 8 packets per
@@ -1161,42 +1091,23 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             uint4* ws, hipStream_t stream, uint64_t slot_bytes) {
+                             hipStream_t stream, uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
+    const FwdArgs fa = {nh, table, table_n};
     if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes) {
         // short frames: 8-lane rows, 8 packets per one-wave workgroup (packet-rate bound, §5g)
-        const FwdArgs fa = {nh, table, table_n};
         hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, true, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0,
                            stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr,
                            (nfcs_patch*)nullptr, fa);
         return hipGetLastError();
     }
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
-    // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower). Bursts of at most
-    // kInlineMaxPackets (or without a workspace) store inline from one kernel; larger ones defer
-    // the stores of their long-frame waves to apply_fwd_kernel, in sub-batches of
-    // kSubBatchPackets above kSubBatchAbovePackets, as the plain update does.
-    if (!ws || n <= kInlineMaxPackets) {
-        const FwdArgs fa = {nh, table, table_n};
-        hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_INLINE>), dim3((n + 15u) / 16u),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, 0u, status,
-                           (nfcs_patch*)nullptr, (nfcs_patch*)nullptr, fa);
-        return hipGetLastError();
-    }
-    const uint32_t sub = n > kSubBatchAbovePackets ? kSubBatchPackets : n;
-    for (uint32_t i = 0; i < n; i += sub) {
-        const uint32_t m = std::min(sub, n - i);
-        const FwdArgs fa = {nh + i, table, table_n};
-        hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_DEFER>), dim3((m + 15u) / 16u),
-                           dim3(kBlock), 0, stream, arena, arena_bytes, desc + i, m, 0u,
-                           status ? status + i : nullptr, (nfcs_patch*)nullptr, (nfcs_patch*)ws, fa);
-        hipLaunchKernelGGL(apply_fwd_kernel, dim3((uint32_t)(((uint64_t)m * 8u + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, stream, arena, desc + i, m, nh + i, table, (const uint4*)ws);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
+    hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_INLINE>), dim3((n + 15u) / 16u),
+                       dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, 0u, status,
+                       (nfcs_patch*)nullptr, (nfcs_patch*)nullptr, fa);
+    return hipGetLastError();
 }
 
 // ---- VLAN push / pop + checksum ----------------------------------------------
