@@ -455,7 +455,14 @@ size_t ChecksumEngine::gather(Pkt* const* pkts, size_t n, size_t limit) {
         copy(0, n);
     } else {
         std::vector<std::thread> th;
-        for (size_t t = 0; t < nt; ++t) th.emplace_back(copy, n * t / nt, n * (t + 1) / nt);
+        th.reserve(nt);
+        for (size_t t = 0; t < nt; ++t) {
+            try {
+                th.emplace_back(copy, n * t / nt, n * (t + 1) / nt);
+            } catch (...) {  // no thread to be had: copy that range here (never throw)
+                copy(n * t / nt, n * (t + 1) / nt);
+            }
+        }
         for (auto& t : th) t.join();
     }
     return off;
