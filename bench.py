@@ -45,8 +45,9 @@ import netflow_amd as nf  # noqa: E402  (loads no library and touches no GPU unt
 
 SEED = 20250620
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip parameters)
-# measured on the MI355X box (tools/stream_read.hip, tools/stream_rw.hip; profiles/r01_stream_microbench.md):
-STREAM_READ_GBPS = 7007.0  # best read-only stream (nt loads)
+# round 1's best read-only stream on the MI355X box (tools/stream_read.hip, nt loads;
+# profiles/r01_stream_microbench.md); the line's stream_ceiling is measured in each run
+STREAM_READ_GBPS = 7007.0
 DEFAULT_PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 C4_PACKETS_PER_GPU = 1 << 22
 FRESH_BATCHES = 4
@@ -67,6 +68,20 @@ def dist_env():
     return ws, rank, local
 
 
+class stdout_to_stderr:
+    """Point file descriptor 1 at stderr for a block (C++ libraries write to it directly)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class Dist:
     """Barrier + max/sum over ranks; a no-op at world size 1. Only the timing barriers and a few
     scalars cross ranks — the data path has no collective — so they go over gloo
@@ -81,8 +96,12 @@ class Dist:
             backend = os.environ.get("NFCS_DIST_BACKEND") or "gloo"
             if backend == "nccl":
                 torch.cuda.set_device(int(os.environ.get("NFCS_BENCH_DEVICE", local)))
-            dist.init_process_group(backend=backend)
             self.dist, self.torch, self.backend = dist, torch, backend
+            # gloo's connection log goes to the process's stdout ("[Gloo] Rank r is connected to
+            # ..."): route fd 1 to stderr while the group forms, so stdout carries only the line
+            with stdout_to_stderr():
+                dist.init_process_group(backend=backend)
+                self.barrier()
 
     def _t(self, v, dtype=None):
         t = self.torch.tensor([v], dtype=dtype or self.torch.float64)
@@ -574,9 +593,17 @@ def main():
         out["bytes"] = {"frame_GBps": round(total_frame_bytes / t_step / 1e9, 2),
                         "checksummed_GBps": round(csum_bytes / t_step / 1e9, 2),
                         "algorithmic_GBps_kernel": round(achieved, 1)}
-        out["stream_ceiling"] = {"read_only_GBps": STREAM_READ_GBPS,
-                                 "frac_of_read_only": round(achieved / STREAM_READ_GBPS, 4),
-                                 "source": "profiles/r01_stream_microbench.md"}
+        # the read-only stream ceiling measured here, on this GPU and over this batch's arena
+        # (nfcs_time_stream_read, both forms; the faster is the reference)
+        it = max(args.steps, 5)
+        sr = [nbytes / (eng.time_stream_read(d_arena, nbytes, it, form=f) / it * 1e-3) / 1e9 for f in (0, 1)]
+        ceil = max(sr)
+        out["stream_ceiling"] = {"read_only_GBps": round(ceil, 1),
+                                 "frac_of_read_only": round(achieved / ceil, 4),
+                                 "read_pass_shape_GBps": round(sr[0], 1), "strided_512wg_GBps": round(sr[1], 1),
+                                 "source": "measured in this run: nfcs_time_stream_read over the batch's "
+                                           f"{nbytes / 1e9:.3f} GB arena, {it} launches per form, HIP events",
+                                 "round1_microbench_GBps": STREAM_READ_GBPS}
     if fresh is not None:
         out["fresh"] = fresh
     if rank == 0 and ws == 1 and not args.no_cpu:

@@ -103,6 +103,7 @@ def _declare(L):
         "nfcs_time_vlan_device": ([_vp, _vp, _u64, _vp, _u32, _u32, _u32, _u32, _vp, ctypes.c_int,
                                    _vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
+        "nfcs_time_stream_read": ([_vp, _vp, _u64, ctypes.c_int, ctypes.c_int, _vp, _vp], ctypes.c_int),
         "nfcs_time_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, ctypes.c_int, _vp,
                                         ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_time_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp,
@@ -324,6 +325,15 @@ class Engine:
         _check(lib().nfcs_time_flow_keys_device(self.ctx, ptr(arena), arena_bytes, ptr(desc), n,
                                                 ptr(keys), ptr(hashes), iters, stream,
                                                 ctypes.byref(ms)), "time_flow_keys_device")
+        return float(ms.value)
+
+    def time_stream_read(self, buf, nbytes, iters, form=0, stream=None) -> float:
+        """Total ms of `iters` pure reads of buf's first nbytes (nfcs_time_stream_read): the
+        read-stream reference the bench reports its kernels against."""
+        ms = ctypes.c_float()
+        p = buf.ptr if isinstance(buf, DeviceBuffer) else int(buf)
+        _check(lib().nfcs_time_stream_read(self.ctx, p, nbytes & ~15, form, iters, stream,
+                                           ctypes.byref(ms)), "time_stream_read")
         return float(ms.value)
 
     def time_l3_forward_device(self, arena, arena_bytes, desc, nh, n, table, table_n, iters,

@@ -1574,6 +1574,67 @@ __host__ __device__ inline uint32_t cfg_len(int config, uint64_t seed, uint64_t 
     }
 }
 
+// ---- read-stream reference (bench support; SURVEY.md §8d "achieved fraction of a measured
+// read-only stream kernel on the same box") -------------------------------------------------------
+// A pure read of `bytes` (16-byte multiple) in the checksum read pass's own shape: 256-thread
+// workgroups in the XCD-aware order at 6 waves/SIMD, each wave reading 6 KiB as 6 non-temporal 1 KiB wave-wide
+// loads in flight (lane l: chunks l + 64k), summed into a value that is stored only if it equals
+// an impossible constant (the loads stay live, nothing is written). form 1: the round-1
+// microbenchmark's best form (tools/stream_read.hip: 512 workgroups striding over the buffer, 4
+// non-temporal loads per lane in flight).
+__global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __restrict__ p, uint64_t n16,
+                                                             unsigned long long* __restrict__ sink) {
+    constexpr uint32_t K = 6;
+    const uint64_t w = (uint64_t)xcd_block() * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t base = w * 64u * K + (threadIdx.x & 63u);
+    uint4 v[K];
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint64_t i = base + 64u * k;
+        v[k] = ld16<1>(i < n16 ? p + i : &g_zero16);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    if (acc == 0x9E3779B9u && sink) *sink = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void stream_read_strided_kernel(const uint4* __restrict__ p, uint64_t n16,
+                                                                     unsigned long long* __restrict__ sink) {
+    constexpr uint32_t U = 4;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t acc = 0;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = ld16<1>(p + i + u * stride);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 v = ld16<1>(p + i);
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u && sink) *sink = acc;
+}
+
+hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsigned long long* sink,
+                              hipStream_t stream) {
+    const uint64_t n16 = bytes / 16u;
+    if (n16 == 0) return hipSuccess;
+    if (form == 1) {
+        hipLaunchKernelGGL(stream_read_strided_kernel, dim3(512), dim3(kBlock), 0, stream, (const uint4*)buf,
+                           n16, sink);
+    } else {
+        const uint64_t per_block = 64u * 6u * kWavesPerBlock;
+        // held at 6 waves/SIMD by kRowsLdsPad, as the checksum read pass is
+        hipLaunchKernelGGL(stream_read_kernel, dim3((uint32_t)((n16 + per_block - 1) / per_block)), dim3(kBlock),
+                           kRowsLdsPad, stream, (const uint4*)buf, n16, sink);
+    }
+    return hipGetLastError();
+}
+
 uint32_t config_len(int config, uint64_t seed, uint64_t index) { return cfg_len(config, seed, index); }
 
 // header byte override at frame offset o (o < 64), or -1

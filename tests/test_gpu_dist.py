@@ -34,8 +34,8 @@ def test_two_ranks_one_gpu_bench_line():
            "--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout  # rank 0 only
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # rank 0's line, nothing else
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["config"]["packets_per_gpu"] == 1 << 22
@@ -52,8 +52,8 @@ def test_two_ranks_strong_split_c3():
            "--warmup", "1", "--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert d["parity"]["match"] is True and d["parity"]["all_ranks"] is True
