@@ -320,8 +320,10 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64
 
 /* The read-stream reference the bench compares its kernels with: `iters` pure
  * non-temporal reads of the first `bytes` (16-byte multiple, 16-byte aligned) of d_buf, nothing
- * written; form 0 = the checksum read pass's shape (6 KiB per wave, 6 loads in flight, XCD-aware
- * order), 1 = 512 workgroups striding with 4 loads per lane in flight. Total milliseconds in *ms. */
+ * written; form 0 = the checksum read pass's shape and load policies (6 KiB per wave, 6 loads in
+ * flight, XCD-aware order, the first load default-policy and the rest non-temporal), 1 = 512
+ * workgroups striding with 4 non-temporal loads per lane in flight, 2 = form 0 with every load
+ * non-temporal. Total milliseconds in *ms. */
 NFCS_API int nfcs_time_stream_read(nfcs_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int form,
                                    int iters, void* stream, float* ms);
 /* Same for nfcs_vlan_device with a uniform edit: launches alternate between op_all (even

@@ -822,7 +822,7 @@ NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uin
 
 NFCS_API int nfcs_time_stream_read(nfcs_ctx* c, const uint8_t* d_buf, uint64_t bytes, int form, int iters,
                                    void* stream, float* ms) {
-    if (!c || !ms || iters <= 0 || !d_buf || (form != 0 && form != 1) || ((uintptr_t)d_buf & 15u))
+    if (!c || !ms || iters <= 0 || !d_buf || form < 0 || form > 2 || ((uintptr_t)d_buf & 15u))
         return NFCS_EINVAL;
     DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);

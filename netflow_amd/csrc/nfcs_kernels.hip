@@ -1593,11 +1593,13 @@ __host__ __device__ inline uint32_t cfg_len(int config, uint64_t seed, uint64_t 
 // ---- read-stream reference (bench support; SURVEY.md §8d "achieved fraction of a measured
 // read-only stream kernel on the same box") -------------------------------------------------------
 // A pure read of `bytes` (16-byte multiple) in the checksum read pass's own shape: 256-thread
-// workgroups in the XCD-aware order at 6 waves/SIMD, each wave reading 6 KiB as 6 non-temporal 1 KiB wave-wide
-// loads in flight (lane l: chunks l + 64k), summed into a value that is stored only if it equals
+// workgroups in the XCD-aware order at 6 waves/SIMD, each wave reading 6 KiB as 6 1 KiB wave-wide
+// loads in flight (lane l: chunks l + 64k; the first with the default policy and the rest
+// non-temporal as in the read pass, or form 2 all non-temporal), summed into a value that is stored only if it equals
 // an impossible constant (the loads stay live, nothing is written). form 1: the round-1
 // microbenchmark's best form (tools/stream_read.hip: 512 workgroups striding over the buffer, 4
 // non-temporal loads per lane in flight).
+template <bool MIX>  // MIX: the first load of each wave with the default policy, as the read pass's header slot
 __global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __restrict__ p, uint64_t n16,
                                                              unsigned long long* __restrict__ sink) {
     constexpr uint32_t K = 6;
@@ -1607,7 +1609,8 @@ __global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __rest
 #pragma unroll
     for (uint32_t k = 0; k < K; ++k) {
         const uint64_t i = base + 64u * k;
-        v[k] = ld16<1>(i < n16 ? p + i : &g_zero16);
+        const uint4* a = i < n16 ? p + i : &g_zero16;
+        v[k] = (MIX && k == 0) ? ld16<0>(a) : ld16<1>(a);
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -1644,9 +1647,14 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsi
                            n16, sink);
     } else {
         const uint64_t per_block = 64u * 6u * kWavesPerBlock;
+        const dim3 grid((uint32_t)((n16 + per_block - 1) / per_block));
         // held at 6 waves/SIMD by kRowsLdsPad, as the checksum read pass is
-        hipLaunchKernelGGL(stream_read_kernel, dim3((uint32_t)((n16 + per_block - 1) / per_block)), dim3(kBlock),
-                           kRowsLdsPad, stream, (const uint4*)buf, n16, sink);
+        if (form == 0)
+            hipLaunchKernelGGL(stream_read_kernel<true>, grid, dim3(kBlock), kRowsLdsPad, stream,
+                               (const uint4*)buf, n16, sink);
+        else
+            hipLaunchKernelGGL(stream_read_kernel<false>, grid, dim3(kBlock), kRowsLdsPad, stream,
+                               (const uint4*)buf, n16, sink);
     }
     return hipGetLastError();
 }

@@ -131,12 +131,12 @@ def test_stream_read_reference(engine):
     nbytes = 64 << 20
     host = np.random.default_rng(3).integers(0, 256, size=nbytes, dtype=np.uint8)
     d = engine.alloc(nbytes).upload(host)
-    for form in (0, 1):
+    for form in (0, 1, 2):
         ms = engine.time_stream_read(d, nbytes, 3, form=form)
         assert ms > 0
     assert np.array_equal(d.download(np.uint8, nbytes), host)
     ms = ctypes.c_float()
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr + 8, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL
-    assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 2, 1, None, ctypes.byref(ms)) == EINVAL
+    assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 3, 1, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 0, 0, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, None, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL
