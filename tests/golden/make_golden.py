@@ -513,6 +513,31 @@ def make_flowkey_c1(R):
     print(f"flowkey C1 digests records {dr:016x} hashes {dh:016x}")
 
 
+def make_l3_more(R):
+    """The bench's other fused-forward workloads (bench.py --op l3fwd --config 3 / --packets 4M):
+    the reference's data path (TTL, MACs, update_checksums) over C3's 4M mixed frames and over 4M
+    C1 frames, next hop i % 9 of l3_table() (8 = no route), one forward each."""
+    res = json.load(open(os.path.join(OUT, "configs.json")))
+    table = l3_table()
+    tab = np.ascontiguousarray(table.reshape(-1))
+    M = (1 << 64) - 1
+    out = []
+    for cfg, n in ((3, 1 << 22), (1, 1 << 22)):
+        dout = 0
+        for lo in range(0, n, CHUNK):
+            m = min(CHUNK, n - lo)
+            arena, desc = oracle.gen_config(cfg, CONFIG_SEED, lo, m)
+            nh = ((np.arange(lo, lo + m)) % 9).astype(np.uint32)
+            R.nfref_l3_forward_batch(oracle._ptr(arena), desc.ctypes.data, oracle._ptr(nh, oracle._u32p),
+                                     m, oracle._ptr(tab), 8, 8)
+            dout = (dout + oracle.digest(arena, desc, lo)) & M
+        out.append({"config": cfg, "first": 0, "n": n, "digest_out": f"{dout:016x}"})
+        print(f"l3fwd config {cfg} n {n}: {dout:016x}")
+    res["l3fwd_more"] = out
+    with open(os.path.join(OUT, "configs.json"), "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+
+
 def make_c4(R):
     """C4: 32M x 1500 B IPv4+UDP sharded across 8 GPUs, 4M packets per rank (weak scaling at
     1/2/4/8 GPUs): the reference's digest of every rank's shard."""
@@ -547,5 +572,7 @@ if __name__ == "__main__":
         make_vlan(R)
     if "c4" in what:
         make_c4(R)
+    if "l3_more" in what:
+        make_l3_more(R)
     if "flowkey_c1" in what:
         make_flowkey_c1(R)
