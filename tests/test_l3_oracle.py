@@ -48,3 +48,18 @@ def test_l3_oracle_vs_reference_fresh():
             continue
         r, fw = oracle.ref_l3_forward_frame(f, h)
         assert o == r and bool(st & 0x80) == bool(fw), i
+
+
+def test_l3_oracle_reproduces_c3_bench_digest(oracle_lib):
+    """The reference's digest of one fused forward over C3's 4M mixed frames (configs.json
+    l3fwd_more, bench.py --op l3fwd --config 3), reproduced by the restatement chunk by chunk."""
+    g = json.load(open(os.path.join(GOLD, "configs.json")))
+    want = next(x for x in g["l3fwd_more"] if x["config"] == 3)
+    table = np.frombuffer(bytes.fromhex(g["l3fwd_c1"]["table"]), dtype=np.uint8).reshape(-1, 12)
+    n, chunk, d = want["n"], 1 << 18, 0
+    for lo in range(0, n, chunk):
+        m = min(chunk, n - lo)
+        arena, desc = oracle.gen_config(3, 20250620, lo, m)
+        oracle.l3_forward_batch(arena, desc, (np.arange(lo, lo + m) % 9).astype(np.uint32), table)
+        d = (d + oracle.digest(arena, desc, lo)) % (1 << 64)
+    assert f"{d:016x}" == want["digest_out"]
