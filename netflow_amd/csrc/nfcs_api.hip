@@ -338,6 +338,19 @@ int update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfc
     return NFCS_OK;
 }
 
+// The fused L3 forward on stream st; a burst above kSubBatchAbovePackets defers the stores of its
+// long-frame waves through patch records in the context workspace (one per packet of a sub-batch).
+int l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfcs_desc* d_desc,
+                      const uint32_t* d_nh, uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
+                      uint8_t* d_status, hipStream_t st) {
+    const bool dfr = n > nfcs::kSubBatchAbovePackets;
+    if (dfr) NFCS_HIP(acquire_ws(c, nfcs::kSubBatchPackets, st));
+    NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
+                                     d_status, dfr ? c->ws : nullptr, st, c->slot_bytes));
+    if (dfr) NFCS_HIP(release_ws(c, st));
+    return NFCS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -449,9 +462,8 @@ NFCS_API int nfcs_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t aren
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || !d_nh || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (table_n > 0 && (!d_table || ((uintptr_t)d_table & 3u))) return NFCS_EINVAL;
-    NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
-                                     d_status, pick(c, stream), c->slot_bytes));
-    return NFCS_OK;
+    return l3_forward_device(c, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n, d_status,
+                             pick(c, stream));
 }
 
 NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes,
@@ -776,9 +788,11 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
-    for (int it = 0; it < iters; ++it)
-        NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table,
-                                         table_n, d_status, st, c->slot_bytes));
+    for (int it = 0; it < iters; ++it) {
+        const int rc = l3_forward_device(c, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
+                                         d_status, st);
+        if (rc) return rc;
+    }
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

@@ -79,7 +79,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream, uint64_t slot_bytes = 0);
+                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes = 0);
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,

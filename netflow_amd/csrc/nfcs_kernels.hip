@@ -648,13 +648,15 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //   SF_RECORDS  patch records only, frames untouched (nfcs_update_host: only the records cross
 //               PCIe back).
 enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
+// ip_off of a deferred forward record whose frame is forwarded without an IPv4 checksum field
+constexpr uint32_t kFwdOnly = 0xFFFEu;
 
 // SF_DEFER's decision for the P packets pw .. pw+P-1 (lengths 0 past n), shared by the read pass
 // and apply_bytes_kernel so both pick the same waves.
 DEV bool defer_group(uint32_t lensum, uint32_t P) { return lensum >= P * (uint32_t)kDeferMeanBytes; }
 DEV uint32_t defer_len(uint32_t len) { return len < 0xFFFFu ? len : 0xFFFFu; }
 
-template <int K, int R = 16, bool FWD = false, bool NT = false>
+template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
                      const uint32_t* wmac = nullptr) {
@@ -784,7 +786,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     // session 3, C3 +2%, uniform 1024-byte frames +2.7%; in the long shape it cost 64K-packet
     // bursts of 9000-byte frames 3%, in 8-lane rows IMIX ±1%), then the status byte / patch
     // record from lane 0.
-    auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool stores) {
+    auto emit = [&](bool on, uint32_t st_, uint32_t ipw_, uint32_t l4w_, bool stores, bool recw = true) {
         if (stores && on && rl < 4) {
             const uint32_t w = (rl & 2u) ? l4w_ : ipw_;
             const uint32_t pos = (w & 0xFFFFu) + (rl & 1u);
@@ -795,7 +797,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         }
         if (on && rl == 0) {
             if (status) status[S.p] = (uint8_t)st_;
-            if (rec) {
+            if (rec && recw) {
                 uint2 r;
                 r.x = (ipw_ & 0xFFFFu) | (l4w_ << 16);
                 r.y = (ipw_ >> 16) | (l4w_ & 0xFFFF0000u);
@@ -816,9 +818,17 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             uint32_t last = 1u;
             if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) last = max(last, ((ipw & 0xFFFFu) + 1u) >> 4);
             if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) last = max(last, ((l4w & 0xFFFFu) + 1u) >> 4);
-            if (rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
+            if ((!DFR || frame_stores) && rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
         }
-        emit(S.valid && !slow, st, ipw, l4w, false);
+        // a deferred wave (large bursts, SF_DEFER) leaves the frame alone here: its patch record
+        // goes to apply_fwd_kernel, which re-reads the first 64 bytes and writes them back
+        // forwarded. The record holds the checksum fields; a forwarded frame without an IPv4
+        // checksum (EtherType IPv4 but version nibble != 4: forwarded, update_checksums() a no-op)
+        // gets ip_off kFwdOnly and its TTL offset in the ip bytes; a frame not forwarded, none.
+        emit(S.valid && !slow, st,
+             (DFR && fwd && live && (ipw & 0xFFFFu) == NFCS_PATCH_NONE) ? (kFwdOnly | ((tagged ? 26u : 22u) << 16))
+                                                                         : ipw,
+             l4w, false);
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
@@ -885,7 +895,9 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         }
         if (FWD) st2 |= NFCS_ST_FLAG_FWD;
         // the forward always stores (its header rewrite went out above)
-        emit(slow, st2, ipw2, l4w2, !seq && (FWD || frame_stores));
+        emit(slow, st2, ipw2, l4w2, !seq && (FWD || frame_stores), !(FWD && DFR));
+        // the forward stored everything of an uncommon header here: nothing left for the write pass
+        if (FWD && DFR && rec && slow && rl == 0) ((uint2*)rec)[S.p] = make_uint2(0xFFFFFFFFu, 0u);
     }
 }
 
@@ -957,7 +969,7 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, nh);
     // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
     // workgroups), write-through elsewhere (see row_process)
-    row_process<K, R, FWD, !FWD && R == 16 && BS == 64>(S, rl, rowbase4, status, rec, frame_stores,
+    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER>(S, rl, rowbase4, status, rec, frame_stores,
                                                          fa.table_n, wmac);
 }
 
@@ -1014,6 +1026,59 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
             asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");
         }
     }
+}
+
+// The fused L3 forward's write pass (large bursts, SF_DEFER). Four lanes per packet, one 16-byte
+// chunk of the frame's first 64 bytes each: a packet whose record names an IPv4 checksum field (it
+// was forwarded, with a common header) has its chunks re-read — still in the memory-side cache
+// that the read pass of this sub-batch just brought them into — and written back forwarded: the
+// next hop's MACs in chunk 0, the TTL (read, minus one; ip_off - 2) and the checksum fields from
+// the record, the other bytes as read (a frame never shares a 16-byte chunk with another), as
+// whole 64-byte segments with non-temporal stores. The deferral decision of each aligned group of
+// 4 packets is recomputed from their lengths, as in apply_bytes_kernel.
+__global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__ arena,
+                                                           const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                           const uint32_t* __restrict__ nh,
+                                                           const nfcs_nexthop* __restrict__ table,
+                                                           const nfcs_patch* __restrict__ rec) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t p = t >> 2, g = p & ~3ull;
+    const uint32_t rl = (uint32_t)t & 3u, k = (uint32_t)(p - g);
+    if (p >= n) return;
+    // one round trip: the group's four descriptors, the record and the next hop, all independent
+    // (records of groups that stored inline are stale and ignored)
+    uint4 d01 = make_uint4(0u, 0u, 0u, 0u), d23 = d01;
+    if (g + 4 <= n) {
+        d01 = ((const uint4*)(desc + g))[0];
+        d23 = ((const uint4*)(desc + g))[1];
+    } else {
+        const uint32_t* q = (const uint32_t*)(desc + g);
+        d01 = make_uint4(q[0], q[1], g + 1 < n ? q[2] : 0u, g + 1 < n ? q[3] : 0u);
+        d23 = make_uint4(g + 2 < n ? q[4] : 0u, g + 2 < n ? q[5] : 0u, g + 3 < n ? q[6] : 0u, g + 3 < n ? q[7] : 0u);
+    }
+    const uint2 r = ((const uint2*)rec)[p];
+    const uint32_t h = nh[p];
+    const uint32_t s = defer_len(d01.y) + defer_len(d01.w) + defer_len(d23.y) + defer_len(d23.w);
+    const uint32_t ipo = r.x & 0xFFFFu;
+    const uint32_t off16 = k == 0 ? d01.x : (k == 1 ? d01.z : (k == 2 ? d23.x : d23.z));
+    const uint32_t len = k == 0 ? d01.y : (k == 1 ? d01.w : (k == 2 ? d23.y : d23.w));
+    // not deferred, not forwarded or written by the read pass, or past the frame
+    if (!defer_group(s, 4) || ipo == NFCS_PATCH_NONE || 16u * rl >= len) return;
+    // the second round trip: the chunk (memory-side cache) and, for chunk 0, the next hop's MACs
+    uint4* c = (uint4*)(arena + (uint64_t)off16 * 16u) + rl;
+    uint4 v = *c;
+    if (rl == 0) {
+        const uint32_t* m = (const uint32_t*)(table + h);
+        v.x = m[0];
+        v.y = m[1];
+        v.z = m[2];
+    }
+    const bool ipf = ipo != kFwdOnly;
+    const uint32_t to = ipf ? ipo - 2u : (r.y & 0xFFFFu);  // TTL (l2 + 8): never borrows (it was > 1)
+    if ((to >> 4) == rl) v = put_byte(v, to & 15u, ((comp(v, (to >> 2) & 3u) >> (8u * (to & 3u))) & 0xFFu) - 1u);
+    if (ipf) v = put_field(v, ipo | (r.y << 16), rl);             // IPv4 field first,
+    v = put_field(v, (r.x >> 16) | (r.y & 0xFFFF0000u), rl);      // then L4
+    st16_nt(c, v);
 }
 
 // Workgroup shapes of the checksum read pass, chosen per call from the mean arena footprint per
@@ -1106,7 +1171,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             hipStream_t stream, uint64_t slot_bytes) {
+                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes) {
     (void)di;
     if (n == 0) return hipSuccess;
     const FwdArgs fa = {nh, table, table_n};
@@ -1116,6 +1181,25 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
                            stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr,
                            (nfcs_patch*)nullptr, fa);
         return hipGetLastError();
+    }
+    if (ws && n > kSubBatchAbovePackets && shape_mean(arena_bytes, n, slot_bytes) >= kSmallMeanBytes) {
+        // bursts of long frames larger than the memory-side cache: per 512K-packet sub-batch, a
+        // read pass whose long-frame waves write patch records instead of segments, then
+        // apply_fwd_kernel while the header lines are still cached (4M x 1500 B
+        // 0.681 -> 0.705; mixes like C3, whose waves rarely defer, lose 10% to the sub-batch
+        // launches and stay in one inline launch)
+        for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
+            const uint32_t m = std::min(kSubBatchPackets, n - i);
+            const FwdArgs fs = {nh + i, table, table_n};
+            hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_DEFER>), dim3((m + 15u) / 16u),
+                               dim3(kBlock), 0, stream, arena, arena_bytes, desc + i, m, 0u,
+                               status ? status + i : nullptr, (nfcs_patch*)nullptr, ws, fs);
+            hipLaunchKernelGGL(apply_fwd_kernel, dim3((uint32_t)(((uint64_t)m * 4u + kBlock - 1) / kBlock)),
+                               dim3(kBlock), 0, stream, arena, desc + i, m, nh + i, table, (const nfcs_patch*)ws);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
     // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
