@@ -193,7 +193,10 @@ typedef struct nfcs_nexthop {
  * forwarded are untouched. The control-plane steps (ACL, classification, is_my_ip, route and
  * ARP lookup) stay with the caller and arrive as next-hop indexes.
  *   d_nh     n device-resident u32 next-hop indexes (NFCS_NH_NONE = no route)
- *   d_table  table_n device-resident next hops */
+ *   d_table  table_n device-resident next hops
+ * Launches (speed only): one kernel; a burst of more than 1M long frames runs as 512K-packet
+ * sub-batches whose long-frame waves write their header rewrites in a second pass.
+ * Asynchronous on the stream; d_nh and d_table must stay valid until it completes. */
 NFCS_API int nfcs_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                     const nfcs_desc* d_desc, const uint32_t* d_nh, uint32_t n,
                                     const nfcs_nexthop* d_table, uint32_t table_n,
