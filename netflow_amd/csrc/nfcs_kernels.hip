@@ -1048,7 +1048,7 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
     // one round trip: the group's four descriptors, the record and the next hop, all independent
     // (records of groups that stored inline are stale and ignored)
     uint4 d01 = make_uint4(0u, 0u, 0u, 0u), d23 = d01;
-    if (g + 4 <= n) {
+    if (g + 4 <= n && ((uintptr_t)(desc + g) & 15u) == 0) {  // (descriptors need only 8-byte alignment)
         d01 = ((const uint4*)(desc + g))[0];
         d23 = ((const uint4*)(desc + g))[1];
     } else {

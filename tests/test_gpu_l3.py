@@ -174,3 +174,23 @@ def test_l3_deferred_sub_batches_fuzz_vs_oracle(engine):
     out, st = run_l3(engine, arena, desc, nh, table)
     assert np.array_equal(st, rst)
     assert np.array_equal(out, ref)
+
+
+def test_l3_deferred_misaligned_descriptors(engine):
+    """Descriptors and next hops need only their natural alignment (8 and 4 bytes): the deferred
+    forward over 1.1M C1 frames with both arrays at an address = 8 mod 16, against the oracle."""
+    n = 1_100_001
+    arena, desc = oracle.gen_config(1, 20250620, 0, n, 128)
+    rng = np.random.default_rng(13)
+    table = rng.integers(0, 256, size=(8, 12), dtype=np.uint8)
+    nh = (np.arange(n) % 9).astype(np.uint32)
+    d_arena = engine.alloc(arena.nbytes).upload(arena)
+    d_desc = engine.alloc(desc.nbytes + 16).upload(np.concatenate([np.zeros(8, np.uint8), desc.view(np.uint8)]))
+    d_nh = engine.alloc(4 * n + 16).upload(np.concatenate([np.zeros(2, np.uint32), nh]))
+    d_tab = engine.alloc(table.nbytes).upload(table)
+    d_st = engine.alloc(n)
+    rst = oracle.l3_forward_batch(arena, desc, nh, table)
+    engine.l3_forward_device(d_arena, arena.nbytes, d_desc.ptr + 8, d_nh.ptr + 8, n, d_tab, 8, d_st)
+    engine.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), arena)
