@@ -186,7 +186,7 @@ typedef struct nfcs_nexthop {
 } nfcs_nexthop;
 #define NFCS_NH_NONE 0xFFFFFFFFu
 
-/* Batched data path of the switch's transit-IPv4 forward (switch.hpp:247-294) in one HBM pass:
+/* Batched data path of the switch's transit-IPv4 forward (switch.hpp:247-294) in one HBM read pass:
  * for packet i with L3 EtherType IPv4 and an IPv4 header, TTL <= 1 -> NFCS_ST_TTL_EXPIRED;
  * d_nh[i] >= table_n -> NFCS_ST_NO_ROUTE; else TTL--, dst/src MAC = d_table[d_nh[i]], then
  * Packet::update_checksums(), status = its status | NFCS_ST_FLAG_FWD. Frames that are not
