@@ -1029,10 +1029,10 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
 }
 
 // The fused L3 forward's write pass (large bursts, SF_DEFER). Four lanes per packet, one 16-byte
-// chunk of the frame's first 64 bytes each: a packet whose record names an IPv4 checksum field (it
-// was forwarded, with a common header) has its chunks re-read — still in the memory-side cache
+// chunk of the frame's first 64 bytes each: a packet whose record is set (it was forwarded, with a
+// common header; kFwdOnly: without an IPv4 checksum field) has its chunks re-read — still in the memory-side cache
 // that the read pass of this sub-batch just brought them into — and written back forwarded: the
-// next hop's MACs in chunk 0, the TTL (read, minus one; ip_off - 2) and the checksum fields from
+// next hop's MACs in chunk 0, the TTL (read, minus one; at ip_off - 2) and the checksum fields from
 // the record, the other bytes as read (a frame never shares a 16-byte chunk with another), as
 // whole 64-byte segments with non-temporal stores. The deferral decision of each aligned group of
 // 4 packets is recomputed from their lengths, as in apply_bytes_kernel.
