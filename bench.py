@@ -309,11 +309,11 @@ def load_traffic(config: int, n: int, op: str = "update"):
     the default batch size of the config or, for C1-shaped frames, the 4M-packet C4 shard; None
     otherwise."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
-    shard = config == 1 and op == "update" and n == 1 << 22
+    shard = config == 1 and op in ("update", "l3fwd") and n == 1 << 22
     if not shard and n != DEFAULT_PACKETS[config]:
         return None
     try:
-        return json.load(open(p)).get("C4_shard" if shard else f"C{config}" + ("" if op == "update" else f"_{op}"))
+        return json.load(open(p)).get(("C4_shard" if shard else f"C{config}") + ("" if op == "update" else f"_{op}"))
     except (OSError, ValueError):
         return None
 

@@ -26,7 +26,7 @@ PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 
 # the kernels of one call of the op: nfcs_update_device is the read pass and, for waves of long
 # frames, the write pass (apply_bytes_kernel); per call = the sum of the per-kernel medians
-KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("update_rows_kernel",),
+KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("update_rows_kernel", "apply_fwd_kernel"),
           "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_kernel",)}
 
 
@@ -85,7 +85,8 @@ def main():
             ("" if op == "update" else f"_{op}")
         # launches per call: nfcs_update_device runs a long-frame batch of more than 1M packets
         # as 512K-packet sub-batches (kSubBatchPackets), each its own read pass + write pass
-        sub = -(-P // (1 << 19)) if (op == "update" and P > (1 << 20)) else 1
+        # (the fused forward too, for long frames: read pass + apply_fwd_kernel per sub-batch)
+        sub = -(-P // (1 << 19)) if (op in ("update", "l3fwd") and P > (1 << 20)) else 1
         f = {k: v * sub for k, v in f.items()}
         w = {k: v * sub for k, v in w.items()}
         q = {k: v * sub for k, v in q.items()}
