@@ -114,3 +114,20 @@ def test_gpus_flag_must_match_world_size():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--no-cpu"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_gloo_group_log_stays_off_stdout():
+    """bench.py forms its gloo group with fd 1 pointed at stderr: gloo's "[Gloo] Rank r is
+    connected ..." lines go to stderr, and stdout carries only what the bench prints after."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import os, sys; sys.path.insert(0, %r); import bench\n"
+        "with bench.stdout_to_stderr():\n"
+        "    os.write(1, b'[Gloo] native write\\n'); print('python print', flush=True)\n"
+        "print('{\"line\": 1}')\n" % root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines() == ['{"line": 1}']
+    assert "[Gloo] native write" in r.stderr and "python print" in r.stderr
