@@ -201,6 +201,43 @@ def golden_digest(config: int, first: int, n: int):
     return None
 
 
+def cgroup_cpu_quota():
+    """CPUs of run time the cgroup allows per period (cgroup v2 cpu.max), None if unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def allotted_cpus() -> list:
+    """The CPUs this process may run on, interleaved across NUMA nodes (node0[0], node1[0],
+    node0[1], ...) so that any prefix of the list is spread over every node."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    nodes = {}
+    base = "/sys/devices/system/node"
+    try:
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                for part in open(os.path.join(base, d, "cpulist")).read().strip().split(","):
+                    a, _, b = part.partition("-")
+                    for c in range(int(a), int(b or a) + 1):
+                        nodes[c] = int(d[4:])
+    except (OSError, ValueError):
+        nodes = {}
+    by = {}
+    for c in cpus:
+        by.setdefault(nodes.get(c, 0), []).append(c)
+    lists = [by[k] for k in sorted(by)]
+    out = []
+    for i in range(max(len(x) for x in lists)):
+        out += [x[i] for x in lists if i < len(x)]
+    return out
+
+
 def cpu_info() -> dict:
     model = None
     try:
@@ -214,21 +251,27 @@ def cpu_info() -> dict:
         allotted = len(os.sched_getaffinity(0))
     except AttributeError:
         allotted = os.cpu_count()
-    return {"cpu_model": model, "nproc": allotted, "machine_cpus": os.cpu_count()}
+    nnodes = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node") and d[4:].isdigit()]) \
+        if os.path.isdir("/sys/devices/system/node") else None
+    return {"cpu_model": model, "nproc": allotted, "machine_cpus": os.cpu_count(),
+            "cgroup_cpu_quota": cgroup_cpu_quota(), "numa_nodes": nnodes}
 
 
-def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str = "update",
-                 one_core_seconds: float = 5.0):
+def cpu_baseline(config: int, threads: int = 0, min_seconds: float = 10.0, op: str = "update",
+                 one_core_seconds: float = 5.0, quota_seconds: float = 5.0):
     """The reference's own update_checksums() (oracle/_ref, compiled from /root/reference) on the
-    host cores over a bounded sample of the workload: `threads` std::threads over contiguous slices,
-    then the same on one thread."""
+    host cores over a bounded sample of the workload: by default one std::thread per allotted CPU
+    (every CPU in the process's affinity set, each thread pinned to one, interleaved across NUMA
+    nodes; SURVEY.md §8d "all host cores"), then on one thread, and — when the cgroup grants fewer
+    CPUs of run time than the affinity set holds — on as many threads as the quota."""
     try:
         import oracle
     except Exception as e:  # pragma: no cover
         return {"value": None, "error": repr(e)}
     kind = "reference" if oracle.ref_available() else "port"
     info = cpu_info()
-    threads = max(1, min(threads, info["nproc"] or threads))
+    cpus = allotted_cpus()
+    threads = max(1, min(threads or len(cpus), len(cpus)))
     # at least ~1.2 GB so the sample streams from DRAM like the GPU batch, not from a large L3
     n = {0: 1024, 1: 1 << 20, 2: 1 << 17, 3: 1 << 21}[config]
     arena, desc = oracle.gen_config(config, SEED, 0, n)
@@ -270,8 +313,10 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
             return lambda: L.nfo_l3_forward_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data,
                                                   oracle._ptr(nh, oracle._u32p), n, oracle._ptr(table), 8, None)
         if kind == "reference":
+            import ctypes
             R = oracle.ref()
-            return lambda: R.nfref_update_batch(oracle._ptr(arena), desc.ctypes.data, n, t)
+            cl = (ctypes.c_int * len(cpus))(*cpus)
+            return lambda: R.nfref_update_batch_on(oracle._ptr(arena), desc.ctypes.data, n, t, cl, len(cpus))
         L = oracle.lib()
         return lambda: L.nfo_update_batch(oracle._ptr(arena), arena.nbytes, desc.ctypes.data, n, None, None, t)
 
@@ -295,13 +340,23 @@ def cpu_baseline(config: int, threads: int, min_seconds: float = 10.0, op: str =
 
     port = kind == "port" and op != "update"  # the oracle's other batch entries are single-threaded
     t_all = 1 if port else threads
+    unit, scale = ("Mpkt/s", n / 1e6) if op == "flowkey" else ("GB/s", nbytes / 1e9)
     reps, el = timed(t_all, min_seconds)
     reps1, el1 = timed(1, one_core_seconds)
-    unit, scale = ("Mpkt/s", n / 1e6) if op == "flowkey" else ("GB/s", nbytes / 1e9)
-    return {"value": round(scale * reps / el, 3), "unit": unit, "cores": t_all, "kind": kind,
-            "one_core": round(scale * reps1 / el1, 3), **info,
-            "sample": f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes on "
-                      f"{t_all} threads ({el:.1f} s) and x {reps1} on 1 thread ({el1:.1f} s), g++ -O2"}
+    out = {"value": round(scale * reps / el, 3), "unit": unit, "cores": t_all, "kind": kind,
+           "one_core": round(scale * reps1 / el1, 3), **info}
+    quota = info.get("cgroup_cpu_quota")
+    q = int(quota) if quota else 0
+    note = ""
+    if not port and 1 < q < t_all:
+        repsq, elq = timed(q, quota_seconds)
+        out["at_quota_threads"] = {"threads": q, "value": round(scale * repsq / elq, 3)}
+        note = (f"; the cgroup grants {quota:g} CPUs of run time, so {t_all} threads share that much; "
+                f"{q} threads: x {repsq} passes ({elq:.1f} s)")
+    out["sample"] = (f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes on "
+                     f"{t_all} threads pinned over the allotted CPUs ({el:.1f} s) and x {reps1} on 1 thread "
+                     f"({el1:.1f} s), g++ -O2" + note)
+    return out
 
 
 def load_traffic(config: int, n: int, op: str = "update"):
@@ -335,7 +390,7 @@ def relaunch(n: int) -> int:
     return subprocess.run(cmd).returncode
 
 
-def main():
+def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -352,9 +407,16 @@ def main():
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch sub-line")
+    ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the C4-shard sub-line")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: every CPU in the affinity set)")
+    return ap
+
+
+def main():
+    ap = make_parser()
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -456,18 +518,24 @@ def main():
     eng.sync()
     regen()  # l3fwd: fresh TTLs for the timed steps
 
+    # N > 1, weak scaling: rank 0's shard timed ALONE first (the other ranks wait at the barrier,
+    # their GPUs idle), with the same steps and clock as the concurrent region below, so the line
+    # carries the one-GPU rate of the very workload the N ranks scale
+    solo = None
+    if ws > 1 and scaling == "weak":
+        D.barrier()
+        if rank == 0:
+            solo_t = timed_steps(eng, step, args.steps, regen if l3 else None)
+        D.barrier()
+        solo = D.sum(frame_bytes / (solo_t / args.steps) / 1e9 if rank == 0 else 0.0)
+        regen()
+
     # timed region: barrier + device sync on both sides, max over ranks
     D.barrier()
-    device_sync()
-    eng.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    eng.sync()
-    device_sync()
-    t1 = time.perf_counter()
+    t_rank = timed_steps(eng, step, args.steps)
     D.barrier()
-    wall = D.max(t1 - t0)
+    wall = D.max(t_rank)
+    t0, t1 = 0.0, t_rank
     ms_per_step = wall / args.steps * 1e3
     total_frame_bytes = D.sum(frame_bytes)
     rank_gbps = D.gather(frame_bytes / ((t1 - t0) / args.steps) / 1e9)
@@ -550,6 +618,10 @@ def main():
         fresh = fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc)
 
     traffic = load_traffic(args.config, n, args.op) if args.align == 128 else None
+    # N = 1: the C4 shard (4M x 1500 B, the per-GPU batch of the N > 1 lines) as a sub-line, so the
+    # one-GPU line carries the anchor that the multi-GPU lines scale
+    c4_wanted = (ws == 1 and args.op == "update" and args.config == 1 and not args.packets
+                 and not args.no_c4)
     total_packets = D.sum(float(n))
     out = {
         "metric": ("flow keys + hash_flow per second, batched packets, MI355X" if fk else
@@ -592,6 +664,15 @@ def main():
     }
     if ws > 1:
         out["per_gpu_GBps"] = [round(x, 1) for x in rank_gbps]  # each rank's own rate, this run
+    if solo is not None:
+        # the same shard on one GPU in this run (rank 0, alone), and value / (N x that)
+        out["single_gpu_same_shard_GBps"] = round(solo, 2)
+        out["efficiency"] = round(out["value"] / (ws * solo), 4)
+        out["efficiency_note"] = ("value / (n_gpus x single_gpu_same_shard_GBps): rank 0's shard timed "
+                                  "alone (other ranks idle at the barrier) before the concurrent region, "
+                                  "same steps and wall clock")
+        if os.environ.get("NFCS_BENCH_DEVICE") is not None:
+            out["efficiency_note"] += "; NFCS_BENCH_DEVICE pins every rank to ONE GPU (a rehearsal)"
     if args.op == "update":
         # frame-only and checksummed-only (frame minus its 14-byte L2 header;
         # the synthetic frames are untagged) rates, and the fraction of the read-only stream
@@ -602,28 +683,78 @@ def main():
                         "checksummed_GBps": round(csum_bytes / t_step / 1e9, 2),
                         "algorithmic_GBps_kernel": round(achieved, 1)}
         # the read-only stream ceiling measured here, on this GPU and over this batch's arena
-        # (nfcs_time_stream_read, three forms; the fastest is the reference)
+        # (nfcs_time_stream_read in six forms; the fastest is the ceiling)
         it = max(args.steps, 5)
-        sr = [nbytes / (eng.time_stream_read(d_arena, nbytes, it, form=f) / it * 1e-3) / 1e9 for f in (0, 1, 2)]
-        ceil = max(sr)
+        forms = {0: "read_pass_shape", 1: "strided_512wg_nt", 2: "read_pass_shape_all_nt",
+                 3: "8_loads_per_lane_nt", 4: "16_loads_per_lane_nt", 5: "4_loads_per_lane_nt"}
+        sr = {f: nbytes / (eng.time_stream_read(d_arena, nbytes, it, form=f) / it * 1e-3) / 1e9 for f in forms}
+        ceil = max(sr.values())
         out["stream_ceiling"] = {"read_only_GBps": round(ceil, 1),
                                  "frac_of_read_only": round(achieved / ceil, 4),
-                                 "read_pass_shape_GBps": round(sr[0], 1), "strided_512wg_nt_GBps": round(sr[1], 1),
-                                 "read_pass_shape_all_nt_GBps": round(sr[2], 1),
+                                 "forms_GBps": {forms[f]: round(v, 1) for f, v in sr.items()},
                                  "source": "measured in this run: nfcs_time_stream_read over the batch's "
                                            f"{nbytes / 1e9:.3f} GB arena, {it} launches per form, HIP events",
                                  "round1_microbench_GBps": STREAM_READ_GBPS}
     if fresh is not None:
         out["fresh"] = fresh
+    if c4_wanted:
+        d_arena.free()
+        d_arena = None
+        out["c4_shard"] = c4_shard_line(eng, args)
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    d_arena.free()
+    if d_arena is not None:
+        d_arena.free()
     eng.close()
     D.close()
+
+
+def timed_steps(eng, step, steps: int, regen=None) -> float:
+    """Wall time of `steps` back-to-back steps, bracketed by device syncs (torch's and the
+    engine's stream). `regen` (the fused forward's TTL refresh) runs once, untimed, before."""
+    if regen is not None:
+        regen()
+    device_sync()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    device_sync()
+    return time.perf_counter() - t0
+
+
+def c4_shard_line(eng, args):
+    """BASELINE C4's per-GPU batch — rank 0's shard, packets [0, 4M) of the 1500-byte stream —
+    on this one GPU: warm-up, wall clock over the steps, the kernels' HIP-event time, the
+    reference's digest of that shard (configs.json c4_rank_shards)."""
+    n = C4_PACKETS_PER_GPU
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(1, SEED, 0, n, args.align)
+    frame_bytes = float(hdesc["len"].astype(np.float64).sum())
+    algo_bytes = frame_bytes + 12.0 * n
+    step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
+    steps = max(args.steps // 4, 5)
+    tw = time.perf_counter()
+    done = 0
+    while done < args.warmup or time.perf_counter() - tw < 0.3:
+        step()
+        done += 1
+    eng.sync()
+    dt = timed_steps(eng, step, steps) / steps
+    ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, steps) / steps
+    want = golden_digest(1, 0, n)
+    got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, 0):016x}"
+    d_arena.free()
+    d_desc.free()
+    return {"workload": "C4 shard: rank 0's 4M x 1500 B IPv4+UDP (the per-GPU batch of the N > 1 lines)",
+            "packets": n, "steps": steps, "value": round(frame_bytes / dt / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+            "frac": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "parity": {"digest": got, "reference_digest": want, "match": None if want is None else got == want}}
 
 
 def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc):

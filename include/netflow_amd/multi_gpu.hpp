@@ -27,6 +27,11 @@ public:
     // NFCS_OK, or the first context's error (then no context is kept).
     MultiGpu(const std::vector<int>& devices, std::nothrow_t, int* rc) {
         int e = devices.empty() ? NFCS_EINVAL : NFCS_OK;
+        try {
+            ctx_.reserve(devices.size());  // push_back below then never allocates
+        } catch (...) {
+            e = NFCS_ENOMEM;
+        }
         for (size_t i = 0; i < devices.size() && e == NFCS_OK; ++i) {
             nfcs_ctx* c = nullptr;
             e = nfcs_ctx_create(devices[i], &c);
@@ -51,11 +56,19 @@ public:
         if (ctx_.empty()) return NFCS_EINVAL;
         if (n == 0) return NFCS_OK;
         const uint32_t parts = (uint32_t)ctx_.size();
-        std::vector<uint32_t> b(parts + 1);
+        // the per-call bookkeeping, allocated up front: bad_alloc becomes NFCS_ENOMEM (never throw)
+        std::vector<uint32_t> b;
+        std::vector<int> res;
+        std::vector<std::thread> th;
+        try {
+            b.resize(parts + 1);
+            res.assign(parts, NFCS_OK);
+            th.reserve(parts);
+        } catch (...) {
+            return NFCS_ENOMEM;
+        }
         int rc = nfcs_shard_bytes(h_desc, n, parts, b.data());
         if (rc != NFCS_OK) return rc;
-        std::vector<int> res(parts, NFCS_OK);
-        std::vector<std::thread> th;
         for (uint32_t p = 1; p < parts; ++p) {
             try {
                 th.emplace_back([&, p] { res[p] = run(p, b, h_arena, arena_bytes, h_desc, h_status, flags); });

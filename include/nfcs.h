@@ -326,7 +326,8 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64
  * written; form 0 = the checksum read pass's shape and load policies (6 KiB per wave, 6 loads in
  * flight, XCD-aware order, the first load default-policy and the rest non-temporal), 1 = 512
  * workgroups striding with 4 non-temporal loads per lane in flight, 2 = form 0 with every load
- * non-temporal. Total milliseconds in *ms. */
+ * non-temporal, 3 / 4 / 5 = 8 / 16 / 4 non-temporal loads per lane (8 / 16 / 4 KiB per wave) with
+ * no occupancy cap. Total milliseconds in *ms. */
 NFCS_API int nfcs_time_stream_read(nfcs_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int form,
                                    int iters, void* stream, float* ms);
 /* Same for nfcs_vlan_device with a uniform edit: launches alternate between op_all (even

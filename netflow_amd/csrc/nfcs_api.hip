@@ -41,6 +41,7 @@ struct nfcs_ctx {
     // host pipeline (nfcs_update_host)
     static constexpr int kSlots = 2;
     static constexpr size_t kStageBytes = size_t(64) << 20;  // arena bytes per staging slot
+    bool host_ready = false;  // every staging slot allocated (ensure_host_pipeline)
     hipStream_t hs[kSlots] = {nullptr, nullptr};
     hipEvent_t done[kSlots] = {nullptr, nullptr};
     size_t stage_bytes = 0;   // arena bytes per slot
@@ -233,8 +234,46 @@ void par_memcpy(void* dst, const void* src, size_t bytes, int threads, const cpu
     for (auto& x : th) x.join();
 }
 
+// Frees the host pipeline's streams, events and buffers (also a partly built one).
+void free_host_pipeline(nfcs_ctx* c) {
+    c->host_ready = false;
+    for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
+        if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
+        if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+        (void)hipFree(c->d_arena[s]);
+        (void)hipFree(c->d_desc[s]);
+        (void)hipFree(c->d_status[s]);
+        (void)hipFree(c->d_patch[s]);
+        host_block_free(c->hb[s]);
+        c->hs[s] = nullptr;
+        c->done[s] = nullptr;
+        c->d_arena[s] = nullptr;
+        c->d_desc[s] = nullptr;
+        c->d_status[s] = nullptr;
+        c->d_patch[s] = nullptr;
+        c->h_arena[s] = nullptr;
+        c->h_desc[s] = nullptr;
+        c->h_status[s] = nullptr;
+        c->h_patch[s] = nullptr;
+    }
+}
+
+int build_host_pipeline(nfcs_ctx* ctx);
+
+// The host pipeline, built on first use on the context's device (the caller holds a DeviceGuard).
+// A build that fails part-way is torn down, so the next call retries it instead of using half of it.
 int ensure_host_pipeline(nfcs_ctx* ctx) {
-    if (ctx->d_arena[0]) return NFCS_OK;
+    if (ctx->host_ready) return NFCS_OK;
+    const int rc = build_host_pipeline(ctx);
+    if (rc != NFCS_OK) {
+        free_host_pipeline(ctx);
+        return rc;
+    }
+    ctx->host_ready = true;
+    return NFCS_OK;
+}
+
+int build_host_pipeline(nfcs_ctx* ctx) {
     ctx->copy_threads = 8;
     ctx->stage_bytes = nfcs_ctx::kStageBytes;
     ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
@@ -304,12 +343,20 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
         const uint32_t m = std::min<uint32_t>(n - i, c->stage_pkts);
         hipStream_t st = c->hs[s];
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        // the launch shape follows this chunk's own frames (their span per packet), not the
+        // caller's whole arena, unless the context has a slot-size hint
+        uint64_t shape = c->slot_bytes;
+        if (!shape) {
+            const uint64_t lo = (uint64_t)h_desc[i].off16 * 16u;
+            const uint64_t hi = (uint64_t)h_desc[i + m - 1].off16 * 16u + (((uint64_t)h_desc[i + m - 1].len + 15u) & ~15ull);
+            shape = hi > lo ? std::max<uint64_t>(1, (hi - lo) / m) : 1;
+        }
         e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                            hipMemcpyHostToDevice, st);
         if (e == hipSuccess)
             e = nfcs::launch_update(c->di, d_arena, arena_bytes, c->d_desc[s], m, 0u,
                                     h_status ? c->d_status[s] : nullptr, nullptr, nullptr,
-                                    nfcs::kUpdateInline, st, c->slot_bytes);
+                                    nfcs::kUpdateInline, st, shape);
         if (e == hipSuccess && h_status)
             e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
@@ -405,15 +452,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     if (!c) return NFCS_OK;
     DeviceGuard dg_(c->di.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
-        if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
-        if (c->done[s]) (void)hipEventDestroy(c->done[s]);
-        (void)hipFree(c->d_arena[s]);
-        (void)hipFree(c->d_desc[s]);
-        (void)hipFree(c->d_status[s]);
-        (void)hipFree(c->d_patch[s]);
-        host_block_free(c->hb[s]);
-    }
+    free_host_pipeline(c);
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
@@ -434,6 +473,8 @@ NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* c, uint32_t bytes) {
 
 NFCS_API int nfcs_ctx_host_numa(nfcs_ctx* c, int* node, int* local) {
     if (!c || !node || !local) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the pipeline is built on the context's device
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     const int rc = ensure_host_pipeline(c);
     if (rc) return rc;
     *node = c->numa_node;
@@ -836,7 +877,7 @@ NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* c, const uint8_t* d_arena, uin
 
 NFCS_API int nfcs_time_stream_read(nfcs_ctx* c, const uint8_t* d_buf, uint64_t bytes, int form, int iters,
                                    void* stream, float* ms) {
-    if (!c || !ms || iters <= 0 || !d_buf || form < 0 || form > 2 || ((uintptr_t)d_buf & 15u))
+    if (!c || !ms || iters <= 0 || !d_buf || form < 0 || form > 5 || ((uintptr_t)d_buf & 15u))
         return NFCS_EINVAL;
     DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);

@@ -648,8 +648,19 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //   SF_RECORDS  patch records only, frames untouched (nfcs_update_host: only the records cross
 //               PCIe back).
 enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
-// ip_off of a deferred forward record whose frame is forwarded without an IPv4 checksum field
-constexpr uint32_t kFwdOnly = 0xFFFEu;
+// The fused forward's deferred record (large bursts, SF_DEFER; the write pass apply_fwd_kernel is
+// its only reader), 8 bytes for a forwarded frame with a common header, all offsets below 64:
+//   x = ip_off | ttl' << 8 | proto << 16 | l4_off << 24, y = ip checksum bytes | l4 checksum bytes << 16
+// ip_off 0xFE: forwarded without an IPv4 checksum field (EtherType IPv4, version nibble != 4:
+// update_checksums() is a no-op), the TTL offset then in y's low byte; l4_off 0xFF: no L4 field;
+// x = 0xFFFFFFFF: nothing for the write pass (not forwarded, or written by the read pass's cold path).
+constexpr uint32_t kFwdNoIp = 0xFEu, kFwdNone = 0xFFu;
+DEV uint2 fwd_record(uint32_t ipw, uint32_t l4w, uint32_t ttl_new, uint32_t proto, bool tagged) {
+    const bool ip = (ipw & 0xFFFFu) != NFCS_PATCH_NONE, l4 = (l4w & 0xFFFFu) != NFCS_PATCH_NONE;
+    const uint32_t ipo = ip ? (ipw & 0xFFu) : kFwdNoIp, l4o = l4 ? (l4w & 0xFFu) : kFwdNone;
+    const uint32_t y = (ip ? (ipw >> 16) : (tagged ? 26u : 22u)) | (l4w & 0xFFFF0000u);
+    return make_uint2(ipo | ((ttl_new & 0xFFu) << 8) | ((proto & 0xFFu) << 16) | (l4o << 24), y);
+}
 
 // SF_DEFER's decision for the P packets pw .. pw+P-1 (lengths 0 past n), shared by the read pass
 // and apply_bytes_kernel so both pick the same waves.
@@ -659,7 +670,7 @@ DEV uint32_t defer_len(uint32_t len) { return len < 0xFFFFu ? len : 0xFFFFu; }
 template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
-                     const uint32_t* wmac = nullptr) {
+                     const uint32_t* wmac = nullptr, const nfcs_nexthop* table = nullptr) {
     const uint32_t len = S.len;
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
@@ -668,7 +679,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
     // rewrite applied to the header registers, so the checksums below see the new header.
     bool fwd = false, tagged = false;
-    uint32_t fst = NFCS_ST_NONE, ttl = 0;
+    uint32_t fst = NFCS_ST_NONE, ttl = 0, proto = 0;
     if (FWD) {
         const RowHdr<R> h{h0, rowbase4};
         const uint32_t e12 = h.be16(12);
@@ -676,11 +687,12 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         const uint32_t l3t = len < 14 ? 0u : (tagged ? (len >= 18 ? h.be16(16) : e12) : e12);
         const bool v4 = l3t == 0x0800u && (tagged ? 38u : 34u) <= len;  // ipv4() present
         ttl = tagged ? h.b(26) : h.b(22);
+        if (DFR) proto = tagged ? h.b(27) : h.b(23);  // the byte beside the TTL (the write pass's TTL short)
         fst = !v4 ? (uint32_t)NFCS_ST_NOT_IPV4
                   : (ttl <= 1 ? (uint32_t)NFCS_ST_TTL_EXPIRED
                               : (S.nh >= table_n ? (uint32_t)NFCS_ST_NO_ROUTE : 0u));
         fwd = live && fst == 0;
-        if (fwd && rl == 0) {  // dst_mac, src_mac (286-289): the row's pick of the wave's MACs
+        if (fwd && rl == 0 && (!DFR || frame_stores)) {  // dst_mac, src_mac (286-289): the row's pick of the wave's MACs
             constexpr uint32_t PW = 64 / R;
             const uint32_t row = rowbase4 / (4u * R);
             uint32_t m0 = 0, m1 = 0, m2 = 0;
@@ -820,15 +832,12 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) last = max(last, ((l4w & 0xFFFFu) + 1u) >> 4);
             if ((!DFR || frame_stores) && rl <= last && 16u * rl < len) st16<true>((uint4*)frame + rl, v);
         }
-        // a deferred wave (large bursts, SF_DEFER) leaves the frame alone here: its patch record
-        // goes to apply_fwd_kernel, which re-reads the first 64 bytes and writes them back
-        // forwarded. The record holds the checksum fields; a forwarded frame without an IPv4
-        // checksum (EtherType IPv4 but version nibble != 4: forwarded, update_checksums() a no-op)
-        // gets ip_off kFwdOnly and its TTL offset in the ip bytes; a frame not forwarded, none.
-        emit(S.valid && !slow, st,
-             (DFR && fwd && live && (ipw & 0xFFFFu) == NFCS_PATCH_NONE) ? (kFwdOnly | ((tagged ? 26u : 22u) << 16))
-                                                                         : ipw,
-             l4w, false);
+        // a deferred wave (large bursts, SF_DEFER) leaves the frame alone here: its forward record
+        // (fwd_record) goes to apply_fwd_kernel, which writes the rewritten bytes without reading
+        // the frame again
+        emit(S.valid && !slow, st, ipw, l4w, false, !DFR);
+        if (DFR && rec && S.valid && !slow && rl == 0)
+            ((uint2*)rec)[S.p] = (fwd && live) ? fwd_record(ipw, l4w, ttl - 1u, proto, tagged) : make_uint2(0xFFFFFFFFu, 0u);
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
@@ -845,10 +854,15 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
                 constexpr uint32_t PW = 64 / R;
                 const uint32_t row = rowbase4 / (4u * R);
                 uint32_t m[3] = {0, 0, 0};
+                if (DFR && !frame_stores) {  // a deferring wave loaded no MACs: this row's, from the table
 #pragma unroll
-                for (uint32_t i = 0; i < PW; ++i) {
+                    for (uint32_t j = 0; j < 3; ++j) m[j] = ((const uint32_t*)(table + S.nh))[j];
+                } else {
 #pragma unroll
-                    for (uint32_t j = 0; j < 3; ++j) m[j] = (row == i) ? wmac[3 * i + j] : m[j];
+                    for (uint32_t i = 0; i < PW; ++i) {
+#pragma unroll
+                        for (uint32_t j = 0; j < 3; ++j) m[j] = (row == i) ? wmac[3 * i + j] : m[j];
+                    }
                 }
 #pragma unroll
                 for (uint32_t j = 0; j < 3; ++j)
@@ -923,6 +937,19 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     if (pw >= n) return;
     // the wave's PW descriptors: one scalar load (s_load_dwordx8 for PW = 4)
     const DescW<PW> D = load_descw<PW>(desc, pw, n);
+    // the store form of each aligned group of 4 packets, from their own frame lengths (scalar
+    // arithmetic on the descriptors): the whole wave with 16-lane rows, each half of the wave with
+    // 8-lane rows; apply_bytes_kernel recomputes the same groups
+    bool defer = false;
+    if (SF == SF_DEFER) {
+        static_assert(PW == 4 || PW == 8, "deferral groups of 4 packets");
+        uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) s0 += defer_len(D.w[2 * i + 1]);
+#pragma unroll
+        for (uint32_t i = 4; i < PW; ++i) s1 += defer_len(D.w[2 * i + 1]);
+        defer = (PW == 8 && row >= 4) ? defer_group(s1, 4) : defer_group(s0, 4);
+    }
     // Fused L3 forward: the wave's PW next-hop indexes and their table rows are wave-uniform.
     // Read through the constant address space they are scalar loads on lgkmcnt, issued with the
     // descriptors so both arrive in one round trip (as generic loads the compiler made each
@@ -942,26 +969,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
             for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
         }
 #pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) {
-            nh |= (row == i) ? q[i] : 0u;
-            const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i]) : (const cu32*)&g_zero16;
-            wmac[3 * i] = m[0];
-            wmac[3 * i + 1] = m[1];
-            wmac[3 * i + 2] = m[2];
+        for (uint32_t i = 0; i < PW; ++i) nh |= (row == i) ? q[i] : 0u;
+        // a deferring wave's MACs are written by apply_fwd_kernel (the checksums do not cover
+        // them): only waves that store inline load them
+        if (!(SF == SF_DEFER && defer)) {
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) {
+                const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i]) : (const cu32*)&g_zero16;
+                wmac[3 * i] = m[0];
+                wmac[3 * i + 1] = m[1];
+                wmac[3 * i + 2] = m[2];
+            }
         }
-    }
-    // the store form of each aligned group of 4 packets, from their own frame lengths (scalar
-    // arithmetic on the descriptors): the whole wave with 16-lane rows, each half of the wave with
-    // 8-lane rows; apply_bytes_kernel recomputes the same groups
-    bool defer = false;
-    if (SF == SF_DEFER) {
-        static_assert(PW == 4 || PW == 8, "deferral groups of 4 packets");
-        uint32_t s0 = 0, s1 = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) s0 += defer_len(D.w[2 * i + 1]);
-#pragma unroll
-        for (uint32_t i = 4; i < PW; ++i) s1 += defer_len(D.w[2 * i + 1]);
-        defer = (PW == 8 && row >= 4) ? defer_group(s1, 4) : defer_group(s0, 4);
     }
     const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
     nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
@@ -970,7 +989,7 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
     // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
     // workgroups), write-through elsewhere (see row_process)
     row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER>(S, rl, rowbase4, status, rec, frame_stores,
-                                                         fa.table_n, wmac);
+                                                         fa.table_n, wmac, fa.table);
 }
 
 // SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
@@ -1028,57 +1047,79 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
     }
 }
 
-// The fused L3 forward's write pass (large bursts, SF_DEFER). Four lanes per packet, one 16-byte
-// chunk of the frame's first 64 bytes each: a packet whose record is set (it was forwarded, with a
-// common header; kFwdOnly: without an IPv4 checksum field) has its chunks re-read — still in the memory-side cache
-// that the read pass of this sub-batch just brought them into — and written back forwarded: the
-// next hop's MACs in chunk 0, the TTL (read, minus one; at ip_off - 2) and the checksum fields from
-// the record, the other bytes as read (a frame never shares a 16-byte chunk with another), as
-// whole 64-byte segments with non-temporal stores. The deferral decision of each aligned group of
-// 4 packets is recomputed from their lengths, as in apply_bytes_kernel.
+// A 2-byte store past the caches (`sc0 sc1 nt`), as st8_nt.
+DEV void st16b_nt(uint8_t* p, uint32_t v) {
+    asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+
+// The fused L3 forward's write pass (large bursts, SF_DEFER), from the records alone — no frame
+// byte is read again. One thread per packet loads its descriptor, record and next hop (coalesced)
+// and, for a forwarded packet of a deferring group of 4 (the decision recomputed from the four
+// lengths, as in apply_bytes_kernel), its next hop's MACs. Then 16 rounds of 4 packets: in round k
+// the 16 lanes of row r write packet 4k + r (its values by ds_bpermute) as ONE instruction of 2-byte
+// stores — lanes 0-5 the MACs (switch.hpp:286-289), lane 6 the TTL with the protocol byte beside it
+// (279), lane 7 the IPv4 checksum, lane 8 an even-offset L4 checksum — so each packet's bytes leave
+// as one write request with a byte mask, past the caches (`sc0 sc1 nt`); an L4 field at an odd
+// offset (TCP: l4 + 15, the 19-byte TcpHeader) goes out as two byte stores after it.
 __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__ arena,
                                                            const nfcs_desc* __restrict__ desc, uint32_t n,
                                                            const uint32_t* __restrict__ nh,
                                                            const nfcs_nexthop* __restrict__ table,
                                                            const nfcs_patch* __restrict__ rec) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t p = t >> 2, g = p & ~3ull;
-    const uint32_t rl = (uint32_t)t & 3u, k = (uint32_t)(p - g);
-    if (p >= n) return;
-    // one round trip: the group's four descriptors, the record and the next hop, all independent
-    // (records of groups that stored inline are stale and ignored)
-    uint4 d01 = make_uint4(0u, 0u, 0u, 0u), d23 = d01;
-    if (g + 4 <= n && ((uintptr_t)(desc + g) & 15u) == 0) {  // (descriptors need only 8-byte alignment)
-        d01 = ((const uint4*)(desc + g))[0];
-        d23 = ((const uint4*)(desc + g))[1];
-    } else {
-        const uint32_t* q = (const uint32_t*)(desc + g);
-        d01 = make_uint4(q[0], q[1], g + 1 < n ? q[2] : 0u, g + 1 < n ? q[3] : 0u);
-        d23 = make_uint4(g + 2 < n ? q[4] : 0u, g + 2 < n ? q[5] : 0u, g + 3 < n ? q[6] : 0u, g + 3 < n ? q[7] : 0u);
-    }
-    const uint2 r = ((const uint2*)rec)[p];
-    const uint32_t h = nh[p];
-    const uint32_t s = defer_len(d01.y) + defer_len(d01.w) + defer_len(d23.y) + defer_len(d23.w);
-    const uint32_t ipo = r.x & 0xFFFFu;
-    const uint32_t off16 = k == 0 ? d01.x : (k == 1 ? d01.z : (k == 2 ? d23.x : d23.z));
-    const uint32_t len = k == 0 ? d01.y : (k == 1 ? d01.w : (k == 2 ? d23.y : d23.w));
-    // not deferred, not forwarded or written by the read pass, or past the frame
-    if (!defer_group(s, 4) || ipo == NFCS_PATCH_NONE || 16u * rl >= len) return;
-    // the second round trip: the chunk (memory-side cache) and, for chunk 0, the next hop's MACs
-    uint4* c = (uint4*)(arena + (uint64_t)off16 * 16u) + rl;
-    uint4 v = *c;
-    if (rl == 0) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool in = i < n;
+    const nfcs_desc d = in ? desc[i] : nfcs_desc{0u, 0u};
+    const uint2 r0 = in ? ((const uint2*)rec)[i] : make_uint2(0xFFFFFFFFu, 0u);
+    const uint32_t h = in ? nh[i] : 0u;
+    uint32_t s = defer_len(d.len);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
+    // records of groups that stored inline are stale: ignored
+    const bool go = in && defer_group(s, 4) && (r0.x & 0xFFu) != kFwdNone;
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(go);
+    if (!mask) return;
+    uint32_t m0 = 0, m1 = 0, m2 = 0;
+    if (go) {  // a forwarded packet's next hop is in the table (the read pass checked it)
         const uint32_t* m = (const uint32_t*)(table + h);
-        v.x = m[0];
-        v.y = m[1];
-        v.z = m[2];
+        m0 = m[0];
+        m1 = m[1];
+        m2 = m[2];
     }
-    const bool ipf = ipo != kFwdOnly;
-    const uint32_t to = ipf ? ipo - 2u : (r.y & 0xFFFFu);  // TTL (l2 + 8): never borrows (it was > 1)
-    if ((to >> 4) == rl) v = put_byte(v, to & 15u, ((comp(v, (to >> 2) & 3u) >> (8u * (to & 3u))) & 0xFFu) - 1u);
-    if (ipf) v = put_field(v, ipo | (r.y << 16), rl);             // IPv4 field first,
-    v = put_field(v, (r.x >> 16) | (r.y & 0xFFFF0000u), rl);      // then L4
-    st16_nt(c, v);
+    const uint32_t rx = go ? r0.x : 0xFFFFFFFFu, ry = r0.y;
+    const uint32_t j = lane & 15u;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        if (((mask >> (4u * k)) & 0xFu) == 0) continue;  // wave-uniform
+        const int q4 = (int)((4u * k + (lane >> 4)) * 4u);  // source lane, in bytes
+        const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)rx);
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)ry);
+        const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d.off16);
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)m0);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)m1);
+        const uint32_t a2 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)m2);
+        const uint32_t ipo = x & 0xFFu, l4o = x >> 24;
+        if (ipo == kFwdNone) continue;
+        uint8_t* f = arena + (uint64_t)o16 * 16u;
+        const uint32_t mw = j < 2 ? a0 : (j < 4 ? a1 : a2);
+        uint32_t off = 0xFFFFu, v = 0;
+        if (j < 6) {
+            off = 2u * j;
+            v = mw >> (16u * (j & 1u));
+        } else if (j == 6) {  // TTL and protocol (l2 + 8, l2 + 9)
+            off = ipo == kFwdNoIp ? (y & 0xFFu) : ipo - 2u;
+            v = ((x >> 8) & 0xFFu) | (((x >> 16) & 0xFFu) << 8);
+        } else if (j == 7 && ipo != kFwdNoIp) {
+            off = ipo;
+            v = y;
+        } else if (j == 8 && l4o != kFwdNone && !(l4o & 1u)) {
+            off = l4o;
+            v = y >> 16;
+        }
+        if (off != 0xFFFFu) st16b_nt(f + off, v & 0xFFFFu);
+        if ((j == 8 || j == 9) && l4o != kFwdNone && (l4o & 1u))
+            st8_nt(f + l4o + (j - 8u), (y >> (16u + 8u * (j - 8u))) & 0xFFu);
+    }
 }
 
 // Workgroup shapes of the checksum read pass, chosen per call from the mean arena footprint per
@@ -1194,8 +1235,8 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
             hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_DEFER>), dim3((m + 15u) / 16u),
                                dim3(kBlock), 0, stream, arena, arena_bytes, desc + i, m, 0u,
                                status ? status + i : nullptr, (nfcs_patch*)nullptr, ws, fs);
-            hipLaunchKernelGGL(apply_fwd_kernel, dim3((uint32_t)(((uint64_t)m * 4u + kBlock - 1) / kBlock)),
-                               dim3(kBlock), 0, stream, arena, desc + i, m, nh + i, table, (const nfcs_patch*)ws);
+            hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
+                               desc + i, m, nh + i, table, (const nfcs_patch*)ws);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -1676,17 +1717,21 @@ __host__ __device__ inline uint32_t cfg_len(int config, uint64_t seed, uint64_t 
 
 // ---- read-stream reference (bench support; SURVEY.md §8d "achieved fraction of a measured
 // read-only stream kernel on the same box") -------------------------------------------------------
-// A pure read of `bytes` (16-byte multiple) in the checksum read pass's own shape: 256-thread
-// workgroups in the XCD-aware order at 6 waves/SIMD, each wave reading 6 KiB as 6 1 KiB wave-wide
-// loads in flight (lane l: chunks l + 64k; the first with the default policy and the rest
-// non-temporal as in the read pass, or form 2 all non-temporal), summed into a value that is stored only if it equals
-// an impossible constant (the loads stay live, nothing is written). form 1: the round-1
-// microbenchmark's best form (tools/stream_read.hip: 512 workgroups striding over the buffer, 4
-// non-temporal loads per lane in flight).
-template <bool MIX>  // MIX: the first load of each wave with the default policy, as the read pass's header slot
+// Pure reads of `bytes` (16-byte multiple), summed into a value that is stored only if it equals an
+// impossible constant (the loads stay live, nothing is written). The bench times every form over the
+// batch's own arena and takes the fastest as the ceiling:
+//   form 0  the checksum read pass's own shape: 256-thread workgroups in the XCD-aware order held at
+//           6 waves/SIMD, each wave reading 6 KiB as 6 wave-wide 1 KiB loads in flight (lane l:
+//           chunks l + 64k), the first with the default policy and the rest non-temporal;
+//   form 2  the same, every load non-temporal;
+//   form 3  8 loads per lane (8 KiB per wave), all non-temporal, no occupancy cap;
+//   form 4  16 loads per lane (16 KiB per wave), all non-temporal, no occupancy cap;
+//   form 5  4 loads per lane (4 KiB per wave), all non-temporal, no occupancy cap;
+//   form 1  round 1's microbenchmark (tools/stream_read.hip): 512 workgroups striding over the
+//           buffer, 4 non-temporal loads per lane in flight.
+template <uint32_t K, bool MIX>  // MIX: the first load of each wave with the default policy
 __global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __restrict__ p, uint64_t n16,
                                                              unsigned long long* __restrict__ sink) {
-    constexpr uint32_t K = 6;
     const uint64_t w = (uint64_t)xcd_block() * kWavesPerBlock + (threadIdx.x >> 6);
     const uint64_t base = w * 64u * K + (threadIdx.x & 63u);
     uint4 v[K];
@@ -1726,19 +1771,16 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsi
                               hipStream_t stream) {
     const uint64_t n16 = bytes / 16u;
     if (n16 == 0) return hipSuccess;
-    if (form == 1) {
-        hipLaunchKernelGGL(stream_read_strided_kernel, dim3(512), dim3(kBlock), 0, stream, (const uint4*)buf,
-                           n16, sink);
-    } else {
-        const uint64_t per_block = 64u * 6u * kWavesPerBlock;
-        const dim3 grid((uint32_t)((n16 + per_block - 1) / per_block));
-        // held at 6 waves/SIMD by kRowsLdsPad, as the checksum read pass is
-        if (form == 0)
-            hipLaunchKernelGGL(stream_read_kernel<true>, grid, dim3(kBlock), kRowsLdsPad, stream,
-                               (const uint4*)buf, n16, sink);
-        else
-            hipLaunchKernelGGL(stream_read_kernel<false>, grid, dim3(kBlock), kRowsLdsPad, stream,
-                               (const uint4*)buf, n16, sink);
+    const uint4* q = (const uint4*)buf;
+    auto grid = [&](uint32_t k) { return dim3((uint32_t)((n16 + 64u * k * kWavesPerBlock - 1) / (64u * k * kWavesPerBlock))); };
+    switch (form) {
+    case 1: hipLaunchKernelGGL(stream_read_strided_kernel, dim3(512), dim3(kBlock), 0, stream, q, n16, sink); break;
+    // forms 0 and 2 are held at 6 waves/SIMD by kRowsLdsPad, as the checksum read pass is
+    case 0: hipLaunchKernelGGL((stream_read_kernel<6, true>), grid(6), dim3(kBlock), kRowsLdsPad, stream, q, n16, sink); break;
+    case 2: hipLaunchKernelGGL((stream_read_kernel<6, false>), grid(6), dim3(kBlock), kRowsLdsPad, stream, q, n16, sink); break;
+    case 3: hipLaunchKernelGGL((stream_read_kernel<8, false>), grid(8), dim3(kBlock), 0, stream, q, n16, sink); break;
+    case 4: hipLaunchKernelGGL((stream_read_kernel<16, false>), grid(16), dim3(kBlock), 0, stream, q, n16, sink); break;
+    default: hipLaunchKernelGGL((stream_read_kernel<4, false>), grid(4), dim3(kBlock), 0, stream, q, n16, sink); break;
     }
     return hipGetLastError();
 }

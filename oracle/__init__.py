@@ -113,6 +113,9 @@ def ref() -> ctypes.CDLL:
         R.nfref_update.restype = None
         R.nfref_update_batch.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
         R.nfref_update_batch.restype = None
+        R.nfref_update_batch_on.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        R.nfref_update_batch_on.restype = None
         R.nfref_struct_sizes.argtypes = [ctypes.c_int]
         R.nfref_struct_sizes.restype = ctypes.c_int
         R.nfref_l3_forward.argtypes = [_u8p, ctypes.c_size_t, _u8p]

@@ -12,6 +12,9 @@
 #include <netflow++/packet.hpp>
 #include <netflow++/packet_classifier.hpp>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <cstdint>
 #include <cstring>
 #include <thread>
@@ -67,6 +70,37 @@ __attribute__((visibility("default"))) void nfref_update_batch(uint8_t* arena, c
         th.emplace_back(work, (uint32_t)((uint64_t)n * t / nthreads),
                         (uint32_t)((uint64_t)n * (t + 1) / nthreads));
     work(0, (uint32_t)((uint64_t)n / nthreads));
+    for (auto& t : th) t.join();
+}
+
+// The same batch with thread t pinned to cpus[t % ncpus] (the bench's CPU baseline: every allotted
+// host CPU, the list interleaved across NUMA nodes by the caller).
+__attribute__((visibility("default"))) void nfref_update_batch_on(uint8_t* arena, const void* desc_v,
+                                                                  uint32_t n, int nthreads,
+                                                                  const int* cpus, int ncpus) {
+    const Desc* desc = static_cast<const Desc*>(desc_v);
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](int t) {
+        if (cpus && ncpus > 0) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpus[t % ncpus], &set);
+            (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+        }
+        const uint32_t lo = (uint32_t)((uint64_t)n * t / nthreads), hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+        Window w;
+        for (uint32_t i = lo; i < hi; ++i) {
+            w.point(arena + (uint64_t)desc[i].off16 * 16, desc[i].len);
+            netflow::Packet pkt(&w.pb);
+            pkt.update_checksums();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+    cpu_set_t saved;
+    const bool restore = pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0;
+    work(0);
+    if (restore) (void)pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
     for (auto& t : th) t.join();
 }
 

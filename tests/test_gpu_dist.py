@@ -42,6 +42,34 @@ def test_two_ranks_one_gpu_bench_line():
     assert d["parity"]["match"] is True and d["parity"]["all_ranks"] is True
     assert d["value"] > 0 and d["roofline"]["kernel_ms"] > 0
     assert len(d["per_gpu_GBps"]) == 2
+    # the same shard on one GPU, timed alone in the same run, and the efficiency against it (both
+    # ranks share cuda:0 here, so about 0.5)
+    assert d["single_gpu_same_shard_GBps"] > 0
+    assert abs(d["efficiency"] - d["value"] / (2 * d["single_gpu_same_shard_GBps"])) < 1e-3
+    assert 0 < d["efficiency"] <= 1.1
+
+
+def test_one_gpu_line_carries_c4_shard_and_all_core_cpu_baseline():
+    """The N = 1 line (C1, BASELINE configs[1]) carries the C4-shard sub-line — the per-GPU batch the
+    N > 1 lines scale, with its own roofline fraction and the reference's digest of that shard — and
+    the CPU baseline on every CPU of the affinity set."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8", "--warmup", "2", "--no-fresh",
+           "--cpu-seconds", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["parity"]["match"] is True
+    c4 = d["c4_shard"]
+    assert c4["packets"] == 1 << 22 and c4["parity"]["match"] is True
+    assert 0.3 < c4["frac"] < 1.0 and c4["value"] > 0
+    cb = d["cpu_baseline"]
+    assert cb["cores"] == cb["nproc"] == len(os.sched_getaffinity(0)) and cb["value"] > 0
+    sc = d["stream_ceiling"]
+    assert sc["read_only_GBps"] == max(sc["forms_GBps"].values())
 
 
 def test_two_ranks_strong_split_c3():

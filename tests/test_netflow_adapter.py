@@ -95,3 +95,31 @@ def test_netflow_packet_vlan_burst_matches_reference(exe):
     r, kv = run(exe, "vgpu", vlan_input(78, 20000))
     assert r.returncode == 0, r.stdout + r.stderr
     assert kv["frames"] == 20000 and kv["mismatches"] == 0 and kv["rc"] == 0
+
+
+def _path_scenario(exe, mode):
+    r = subprocess.run([exe, mode], capture_output=True, text=True, timeout=300)
+    kv = {k: int(v) for k, v in (x.split("=") for x in r.stdout.split("\n", 1)[0].split())}
+    return r, kv
+
+
+def test_reference_path_scenario_cpu(exe):
+    """The reference's own test of the path, PacketTest.UpdateChecksumsAfterModification
+    (tests/packet_test.cpp:202-293): its builder's IPv4/TCP, TCP and UDP frames, update_checksums(),
+    src_ip := 1.2.3.4 and TCP src_port := 54321, update again — through netflow_amd::Packet's
+    single-packet CPU members; its EXPECT_NE conditions hold and every byte equals the reference's
+    per-packet result after each step."""
+    r, kv = _path_scenario(exe, "path-cpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv == {"frames": 3, "steps": 2, "mismatches": 0, "expect_ne_failed": 0, "rc": 0}
+
+
+@pytest.mark.gpu
+def test_reference_path_scenario_gpu_burst(exe):
+    """The same scenario as a burst of 3072 netflow::Packet (the test's three frames, then 1023
+    variants of each) through netflow_amd::update_checksums_batch on the GPU, twice: the reference's
+    EXPECT_NE conditions on every packet, and byte equality with the reference's own per-packet
+    update_checksums() after each step."""
+    r, kv = _path_scenario(exe, "path-gpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv == {"frames": 3072, "steps": 2, "mismatches": 0, "expect_ne_failed": 0, "rc": 0}
