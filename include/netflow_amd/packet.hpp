@@ -547,9 +547,13 @@ int ChecksumEngine::flow_keys_batch(Pkt* const* pkts, size_t n, nfcs_flow_key* k
 // descriptors straight into the arena and calls nfcs_update_host on it (frames DMA'd from the
 // pinned arena, patch records back; or, with NFCS_HOST_ZERO_COPY, read by the kernel over PCIe
 // in place). Buffers larger than a slot are heap PacketBuffers, as the reference allocates them.
+// The default slot is 2176 bytes (a 2048-byte data room + 128 bytes of headroom, DPDK's mbuf
+// layout): power-of-two slots alias on MI355X — C1's frames in 2048-byte slots checksum at 0.716 of
+// 8 TB/s (read pass 232 µs, write pass 41.7 µs) against 0.781 in 2176-byte slots (222 / 28.5 µs;
+// round 3, profiles/r03_stride_*.json).
 class BufferPool {
 public:
-    explicit BufferPool(size_t slots = 65536, size_t slot_bytes = 2048,
+    explicit BufferPool(size_t slots = 65536, size_t slot_bytes = 2176,
                         ChecksumEngine& engine = ChecksumEngine::instance())
         : eng_(engine), slots_(slots), slot_bytes_((slot_bytes + 15) & ~size_t(15)) {
         if (slots_ == 0 || slots_ * slot_bytes_ / 16 > 0xFFFFFFFFull)

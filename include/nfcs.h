@@ -126,12 +126,16 @@ NFCS_API int nfcs_last_hip_error(void);
 NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out);
 NFCS_API int nfcs_ctx_destroy(nfcs_ctx* ctx);
 NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t */
-/* Launch shapes (speed only; the bytes written never depend on them) follow the mean arena bytes
- * per packet, arena_bytes / n: 8-lane rows for short frames, 16-lane rows for long ones, long-frame
- * sub-batches. A caller whose bursts fill a small part of a large arena (a NIC ring) states its
- * frames' mean slot size instead, e.g. 128 for 64-byte frames in 128-byte slots;
- * 0 (the default) restores arena_bytes / n. Applies to the device-path calls that follow on ctx (update, L3 forward,
- * VLAN; nfcs_update_host measures each staged chunk itself). */
+/* Launch shapes (speed only; the bytes written never depend on them) follow the mean footprint per
+ * packet: 8-lane rows for short frames, 16-lane rows for long ones, long-frame sub-batches. Without
+ * a hint it is arena_bytes / n, which is exact for a batch that fills its arena and otherwise only
+ * over-estimates; when that estimate says "long", the update and the L3 forward also sample the
+ * frames' real footprint on the device (256 descriptors, one wave, no host sync), and the next call
+ * on the same descriptor array launches in the shape the sample calls for — a burst inside a larger
+ * ring (a NIC ring reusing its descriptor array) adapts after one call. A caller may
+ * instead state its frames' mean slot size, e.g. 128 for 64-byte frames in 128-byte slots; 0 (the
+ * default) restores the automatic choice. Applies to the device-path calls that follow on ctx
+ * (update, L3 forward, VLAN; nfcs_update_host measures each staged chunk itself). */
 NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* ctx, uint32_t bytes);
 /* The host staging ring of nfcs_update_host (allocated by this call if not yet): *node = the GPU's
  * NUMA node (-1 if unknown), *local = 1 when the ring's pinned memory is bound to that node (its

@@ -65,6 +65,11 @@ struct nfcs_ctx {
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
     uint32_t slot_bytes = 0;  // launch-shape hint (nfcs_ctx_set_slot_bytes); 0 = arena_bytes / n
+    // the footprint observation (launch_shape): host-mapped u32 the kernels write, and the
+    // descriptor array it belongs to
+    uint32_t* obs_host = nullptr;
+    uint32_t* obs_dev = nullptr;
+    const void* obs_desc = nullptr;
 };
 
 namespace {
@@ -374,13 +379,35 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
     return NFCS_OK;
 }
 
+// The launch shape's mean footprint per packet for a device call (speed only; the bytes written
+// never depend on it): the context's slot-size hint when set; else arena_bytes / n, which is exact
+// for a batch that fills its arena and can only over-estimate (frames never overlap). So a short
+// estimate is right, and only a long one can be wrong — a burst inside a larger ring. Then the call
+// also has its launch sample the frames' real footprint (sample_footprint, one wave, host-mapped
+// result), and the next call on the same descriptor array launches in the shape that sample says:
+// a NIC ring reusing its descriptor array adapts after one call, with no hint and no host sync.
+struct Shape { uint64_t mean; uint32_t* obs; };
+Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
+    if (c->slot_bytes) return {c->slot_bytes, nullptr};
+    const uint64_t est = arena_bytes / n;
+    if (est < nfcs::kSmallMeanBytes || !c->obs_host) return {est, nullptr};
+    if (c->obs_desc != d_desc) {  // another descriptor array: its own observation, from this call on
+        c->obs_desc = d_desc;
+        __atomic_store_n(c->obs_host, 0u, __ATOMIC_RELAXED);
+        return {est, c->obs_dev};
+    }
+    const uint32_t o = __atomic_load_n(c->obs_host, __ATOMIC_RELAXED);  // the latest call's sample
+    return {o ? std::min<uint64_t>(o, est) : est, c->obs_dev};
+}
+
 // The device-resident update on stream st: kUpdateAuto, deferred records into the caller's
 // d_patch when given, else into the context workspace.
 int update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfcs_desc* d_desc,
                   uint32_t n, uint8_t* d_status, nfcs_patch* d_patch, hipStream_t st) {
     if (!d_patch) NFCS_HIP(acquire_ws(c, n, st));
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
     NFCS_HIP(nfcs::launch_update(c->di, d_arena, arena_bytes, d_desc, n, 0u, d_status, d_patch,
-                                 d_patch ? nullptr : c->ws, nfcs::kUpdateAuto, st, c->slot_bytes));
+                                 d_patch ? nullptr : c->ws, nfcs::kUpdateAuto, st, sh.mean, sh.obs));
     if (!d_patch) NFCS_HIP(release_ws(c, st));
     return NFCS_OK;
 }
@@ -392,8 +419,9 @@ int l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const
                       uint8_t* d_status, hipStream_t st) {
     const bool dfr = n > nfcs::kSubBatchAbovePackets;
     if (dfr) NFCS_HIP(acquire_ws(c, nfcs::kSubBatchPackets, st));
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
     NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
-                                     d_status, dfr ? c->ws : nullptr, st, c->slot_bytes));
+                                     d_status, dfr ? c->ws : nullptr, st, sh.mean, sh.obs));
     if (dfr) NFCS_HIP(release_ws(c, st));
     return NFCS_OK;
 }
@@ -440,6 +468,11 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->obs_host, 64, hipHostMallocMapped);
+    if (e == hipSuccess) {
+        *c->obs_host = 0;
+        e = hipHostGetDevicePointer((void**)&c->obs_dev, c->obs_host, 0);
+    }
     if (e != hipSuccess) {
         nfcs_ctx_destroy(c);
         return hip_fail(e);
@@ -459,6 +492,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->obs_host) (void)hipHostFree(c->obs_host);
     delete c;
     return NFCS_OK;
 }

@@ -41,10 +41,11 @@ DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((
 // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin; this bijection on
 // [0, gridDim.x) gives each XCD one contiguous eighth of the blocks (the tail beyond a
 // multiple of 8 keeps its order).
-DEV uint32_t xcd_block() {
-    const uint32_t b = blockIdx.x, g8 = gridDim.x / 8u;
+DEV uint32_t xcd_block_n(uint32_t nblocks) {
+    const uint32_t b = blockIdx.x, g8 = nblocks / 8u;
     return b < 8u * g8 ? (b % 8u) * g8 + b / 8u : b;
 }
+DEV uint32_t xcd_block() { return xcd_block_n(gridDim.x); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
 __device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
@@ -597,12 +598,31 @@ struct RowStage {
     uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
 };
 
-// Fused L3 forward inputs (unused by the plain update).
+// Per-launch extras of update_rows_kernel: the fused L3 forward's inputs (unused by the plain
+// update) and the footprint observation slot (sample_footprint; null = none).
 struct FwdArgs {
     const uint32_t* nh;
     const nfcs_nexthop* table;
     uint32_t table_n;
+    uint32_t* obs;
 };
+
+// The mean footprint of a call's frames — 256 descriptors spread evenly over the batch, each length
+// rounded up to 128 bytes — written to *obs (host-mapped, system scope) by one wave of the launch.
+// The next call on the same descriptor array picks its launch shape from it when arena_bytes / n
+// cannot tell (a burst inside a larger ring; nfcs_api.hip update_device). Speed only.
+DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32_t lane, uint32_t* obs) {
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t len = desc[(uint32_t)(((uint64_t)(4u * lane + k) * n) >> 8)].len;
+        s += ((len < 0xFFFFu ? len : 0xFFFFu) + 127u) & ~127u;
+    }
+    s = row_sum<16>(s);
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)s, 0) + (uint32_t)__builtin_amdgcn_readlane((int)s, 16) +
+                       (uint32_t)__builtin_amdgcn_readlane((int)s, 32) + (uint32_t)__builtin_amdgcn_readlane((int)s, 48);
+    if (lane == 0) __hip_atomic_store(obs, (t >> 8) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
@@ -921,20 +941,28 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 // the workgroups one XCD runs take one contiguous eighth of the batch, so each XCD streams its
 // own region of HBM and the descriptor lines its workgroups share stay in its L2 (a bijection on
 // [0, gridDim.x); the tail beyond a multiple of 8 keeps its order). C1 +1.3%, C3 +0.5%.
+// Arguments in the order a wave needs them: the first eight (14 dwords: what every wave reads
+// before its frame loads, plus the footprint slot) are preloaded into SGPRs at dispatch
+// (-amdgpu-kernarg-preload-count=8, netflow_amd/__init__.py), so a wave's first memory access is
+// its descriptor load, with no kernel-argument round trip ahead of it; `nblocks` (= gridDim.x) is
+// passed explicitly for the same reason (the grid size is a hidden argument, loaded from memory).
 template <int K, int R, int OCC, int BS, bool FWD, int SF>
-__global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restrict__ arena,
-                                                              uint64_t arena_bytes,
-                                                              const nfcs_desc* __restrict__ desc,
-                                                              uint32_t n, uint32_t base16,
+__global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                              uint32_t nblocks, uint8_t* __restrict__ arena,
+                                                              uint64_t arena_bytes, uint32_t base16,
+                                                              const uint32_t* __restrict__ nh,
+                                                              uint32_t* __restrict__ obs,
                                                               uint8_t* __restrict__ status,
                                                               nfcs_patch* __restrict__ patch,
                                                               nfcs_patch* __restrict__ ws,
-                                                              FwdArgs fa) {
+                                                              const nfcs_nexthop* __restrict__ table,
+                                                              uint32_t table_n) {
     constexpr uint32_t PW = 64 / R;  // packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = (uint64_t)xcd_block() * (BS / R) + rfl(threadIdx.x >> 6) * PW;
+    const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (BS / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
+    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, n, lane, obs);
     // the wave's PW descriptors: one scalar load (s_load_dwordx8 for PW = 4)
     const DescW<PW> D = load_descw<PW>(desc, pw, n);
     // the store form of each aligned group of 4 packets, from their own frame lengths (scalar
@@ -951,16 +979,15 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
         defer = (PW == 8 && row >= 4) ? defer_group(s1, 4) : defer_group(s0, 4);
     }
     // Fused L3 forward: the wave's PW next-hop indexes and their table rows are wave-uniform.
-    // Read through the constant address space they are scalar loads on lgkmcnt, issued with the
-    // descriptors so both arrive in one round trip (as generic loads the compiler made each
-    // index a vector load drained by vmcnt(0) ahead of the frame loads: four serial memory
-    // round trips per wave).
+    // Read through the constant address space they are scalar loads on lgkmcnt: the indexes are
+    // issued with the descriptors, and everything that depends on them (the row's pick, the MAC
+    // loads) comes after the frame loads are issued (row_stage's sched_barrier), so no frame load
+    // waits for a next-hop round trip (as generic loads the compiler made each index a vector load
+    // drained by vmcnt(0) ahead of the frame loads: four serial memory round trips per wave).
     typedef const __attribute__((address_space(4))) uint32_t cu32;
-    uint32_t nh = 0;
-    uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
+    uint32_t q[PW];
     if (FWD) {
-        const cu32* nhp = (const cu32*)fa.nh + pw;
-        uint32_t q[PW];
+        const cu32* nhp = (const cu32*)nh + pw;
         if (pw + PW <= n) {
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) q[i] = nhp[i];
@@ -968,28 +995,31 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(uint8_t* __restric
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
         }
+    }
+    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
+    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
+    RowStage<K> S;
+    row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, 0u);
+    uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
+    if (FWD) {
 #pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) nh |= (row == i) ? q[i] : 0u;
+        for (uint32_t i = 0; i < PW; ++i) S.nh |= (row == i) ? q[i] : 0u;
         // a deferring wave's MACs are written by apply_fwd_kernel (the checksums do not cover
         // them): only waves that store inline load them
         if (!(SF == SF_DEFER && defer)) {
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) {
-                const cu32* m = (q[i] < fa.table_n) ? (const cu32*)(fa.table + q[i]) : (const cu32*)&g_zero16;
+                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)&g_zero16;
                 wmac[3 * i] = m[0];
                 wmac[3 * i + 1] = m[1];
                 wmac[3 * i + 2] = m[2];
             }
         }
     }
-    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
-    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
-    RowStage<K> S;
-    row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, nh);
     // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
     // workgroups), write-through elsewhere (see row_process)
     row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER>(S, rl, rowbase4, status, rec, frame_stores,
-                                                         fa.table_n, wmac, fa.table);
+                                                         table_n, wmac, table);
 }
 
 // SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
@@ -1133,23 +1163,30 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
 //   kShapeLong   16-lane rows in 256-thread workgroups held at 6 waves/SIMD.
 enum : int { kShapeTiny = 0, kShapeShort = 1, kShapeLong = 2 };
 
+// One launch of update_rows_kernel (the grid size passed as `nblocks` too).
+template <int K, int R, int OCC, int BS, bool FWD, int SF>
+static void launch_rows(uint32_t grid, unsigned lds, hipStream_t stream, uint8_t* arena, uint64_t arena_bytes,
+                        const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status, nfcs_patch* patch,
+                        nfcs_patch* ws, const FwdArgs& fa) {
+    hipLaunchKernelGGL((update_rows_kernel<K, R, OCC, BS, FWD, SF>), dim3(grid), dim3(BS), lds, stream, desc, n, grid,
+                       arena, arena_bytes, base16, fa.nh, fa.obs, status, patch, ws, fa.table, fa.table_n);
+}
+
 // One launch of the checksum path (its read pass and, for kUpdateAuto, its write pass) over n
 // packets, in the shape chosen for the whole call.
 static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
                                     uint32_t base16, uint8_t* status, nfcs_patch* patch, nfcs_patch* ws,
-                                    int form, int shape, hipStream_t stream) {
-    const FwdArgs nofwd = {nullptr, nullptr, 0};
+                                    int form, int shape, hipStream_t stream, uint32_t* obs) {
+    const FwdArgs nofwd = {nullptr, nullptr, 0, obs};
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
-    const dim3 g8((n + 7u) / 8u), g1((n + 3u) / 4u), g4((n + 15u) / 16u);
+    const uint32_t g8 = (n + 7u) / 8u, g1 = (n + 3u) / 4u, g4 = (n + 15u) / 16u;
 #define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
-    hipLaunchKernelGGL((update_rows_kernel<6, 16, OCC, BS, false, SF>), G, dim3(BS),                \
-                       BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc, n, base16,  \
-                       status, patch, ws, nofwd)
-#define NFCS_ROWS8(SF)                                                                             \
-    hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, false, SF>), g8, dim3(64), 0u, stream, arena,  \
-                       arena_bytes, desc, n, base16, status, patch, ws, nofwd)
+    launch_rows<6, 16, OCC, BS, false, SF>(G, BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc, \
+                                           n, base16, status, patch, ws, nofwd)
+#define NFCS_ROWS8(SF) \
+    launch_rows<6, 8, 8, 64, false, SF>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd)
 #define NFCS_SHAPED(SF)                                                                            \
     do {                                                                                           \
         if (shape == kShapeTiny) NFCS_ROWS8(SF);                                                   \
@@ -1178,7 +1215,7 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
-                         uint64_t slot_bytes) {
+                         uint64_t slot_bytes, uint32_t* obs) {
     (void)di;
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
@@ -1201,26 +1238,26 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(kSubBatchPackets, n - i),
                                                    base16, status ? status + i : nullptr,
-                                                   patch ? patch + i : nullptr, ws, form, shape, stream);
+                                                   patch ? patch + i : nullptr, ws, form, shape, stream,
+                                                   i == 0 ? obs : nullptr);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, shape, stream);
+    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, shape, stream, obs);
 }
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes) {
+                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes, uint32_t* obs) {
     (void)di;
     if (n == 0) return hipSuccess;
-    const FwdArgs fa = {nh, table, table_n};
+    const FwdArgs fa = {nh, table, table_n, obs};
     if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes) {
         // short frames: 8-lane rows, 8 packets per one-wave workgroup (packet-rate bound, §5g)
-        hipLaunchKernelGGL((update_rows_kernel<6, 8, 8, 64, true, SF_INLINE>), dim3((n + 7u) / 8u), dim3(64), 0,
-                           stream, arena, arena_bytes, desc, n, 0u, status, (nfcs_patch*)nullptr,
-                           (nfcs_patch*)nullptr, fa);
+        launch_rows<6, 8, 8, 64, true, SF_INLINE>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+                                                  nullptr, nullptr, fa);
         return hipGetLastError();
     }
     if (ws && n > kSubBatchAbovePackets && shape_mean(arena_bytes, n, slot_bytes) >= kSmallMeanBytes) {
@@ -1231,10 +1268,9 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // launches and stay in one inline launch)
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
-            const FwdArgs fs = {nh + i, table, table_n};
-            hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_DEFER>), dim3((m + 15u) / 16u),
-                               dim3(kBlock), 0, stream, arena, arena_bytes, desc + i, m, 0u,
-                               status ? status + i : nullptr, (nfcs_patch*)nullptr, ws, fs);
+            const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};
+            launch_rows<6, 16, 7, kBlock, true, SF_DEFER>((m + 15u) / 16u, 0u, stream, arena, arena_bytes, desc + i, m,
+                                                          0u, status ? status + i : nullptr, nullptr, ws, fs);
             hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
                                desc + i, m, nh + i, table, (const nfcs_patch*)ws);
             const hipError_t e = hipGetLastError();
@@ -1244,9 +1280,8 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     }
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
     // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
-    hipLaunchKernelGGL((update_rows_kernel<6, 16, 7, kBlock, true, SF_INLINE>), dim3((n + 15u) / 16u),
-                       dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, 0u, status,
-                       (nfcs_patch*)nullptr, (nfcs_patch*)nullptr, fa);
+    launch_rows<6, 16, 7, kBlock, true, SF_INLINE>((n + 15u) / 16u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+                                                   nullptr, nullptr, fa);
     return hipGetLastError();
 }
 

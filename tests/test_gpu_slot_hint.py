@@ -86,3 +86,51 @@ def test_vlan_every_shape_matches_oracle(hinted):
         assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), hint
     for b in (d_arena, d_desc, d_ops, d_caps, d_st):
         b.free()
+
+
+def ring_burst(n, L, slot, seed):
+    """n IPv4/UDP frames of L bytes at the starts of `slot`-byte slots (a NIC ring's layout)."""
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, size=(n, slot), dtype=np.uint8)
+    host[:, L:] = 0
+    host[:, 12], host[:, 13], host[:, 14], host[:, 15] = 0x08, 0x00, 0x45, 0x00
+    host[:, 16], host[:, 17] = (L - 14) >> 8, (L - 14) & 0xFF
+    host[:, 22], host[:, 23] = 64, 17
+    host[:, 38], host[:, 39] = (L - 34) >> 8, (L - 34) & 0xFF
+    desc = np.zeros(n, dtype=oracle.DESC_DTYPE)
+    desc["off16"] = np.arange(n, dtype=np.uint32) * (slot // 16)
+    desc["len"] = L
+    return host.reshape(-1), desc
+
+
+def test_ring_burst_adapts_without_hint(engine):
+    """1M 64-byte frames at the start of a 4 GiB ring, NO slot-size hint: arena_bytes / n (4 KiB)
+    says long frames, so the first call runs the long shape and samples the frames' footprint
+    (sample_footprint); from the second call on the same descriptor array the launch runs the shape
+    the sample calls for (8-lane rows), as fast as with the hint. Bytes equal the oracle's at every
+    call (the shape picks speed only)."""
+    n, L, slot, ring = 1 << 20, 64, 128, 4 << 30
+    host, desc = ring_burst(n, L, slot, 7)
+    ref = host.copy()
+    oracle.update_batch(ref, desc, nthreads=8)
+    engine.set_slot_bytes(0)
+    a = engine.alloc(ring)
+    d = engine.alloc(desc.nbytes).upload(desc)
+    try:
+        a.upload(host)
+        first = engine.time_update_device(a, ring, d, n, 1)  # the long shape + the sample
+        engine.sync()
+        assert np.array_equal(a.download(np.uint8, host.nbytes), ref)
+        engine.time_update_device(a, ring, d, n, 10)  # warm
+        adapted = engine.time_update_device(a, ring, d, n, 40) / 40
+        assert np.array_equal(a.download(np.uint8, host.nbytes), ref)  # idempotent (SURVEY Q7)
+        engine.set_slot_bytes(slot)
+        engine.time_update_device(a, ring, d, n, 10)
+        hinted = engine.time_update_device(a, ring, d, n, 40) / 40
+        print(f"1M x 64 B in a 4 GiB ring: first call {first * 1e3:.1f} us, adapted {adapted * 1e3:.1f} us, "
+              f"with the hint {hinted * 1e3:.1f} us")
+        assert adapted < 1.15 * hinted + 0.005  # ms
+    finally:
+        engine.set_slot_bytes(0)
+        a.free()
+        d.free()
