@@ -53,11 +53,18 @@ class NfcsError(RuntimeError):
     pass
 
 
+# The first 8 kernel arguments go into SGPRs at dispatch (gfx950 kernarg preloading): the row
+# kernel orders its arguments so that everything a wave reads before its frame loads is among them
+# (nfcs_kernels.hip, update_rows_kernel). Round 3 A/B on one box: C3 +0.5-0.8%, 1M x 64 B +1.7%,
+# flow keys +1%, C1 / C2 / the fused forward / VLAN within +-0.5% (profiles/r03_s1_ab_kernarg_preload.jsonl).
+KERNARG_PRELOAD = ["-mllvm", "-amdgpu-kernarg-preload-count=8"]
+
+
 def build(verbose: bool = False) -> str:
     """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree). The measurement
     build (extra launch forms for A/B runs) is separate: tools/exp/build.sh."""
     out = os.path.join(HERE, "libnfcs.so")
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", *KERNARG_PRELOAD,
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"), *SOURCES, "-o", out]
     if verbose:
         print(" ".join(cmd))

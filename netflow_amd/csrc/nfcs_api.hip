@@ -551,8 +551,9 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
-                               cap_all, d_status, pick(c, stream), c->slot_bytes));
+                               cap_all, d_status, pick(c, stream), sh.mean, sh.obs));
     return NFCS_OK;
 }
 
@@ -883,10 +884,12 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
-    for (int it = 0; it < iters; ++it)
+    for (int it = 0; it < iters; ++it) {
+        const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
                                    (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
-                                   c->slot_bytes));
+                                   sh.mean, sh.obs));
+    }
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));
     NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));

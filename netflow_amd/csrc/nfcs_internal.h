@@ -86,7 +86,8 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes = 0);
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes = 0,
+                       uint32_t* obs = nullptr);
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,

@@ -1254,13 +1254,25 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     (void)di;
     if (n == 0) return hipSuccess;
     const FwdArgs fa = {nh, table, table_n, obs};
-    if (shape_mean(arena_bytes, n, slot_bytes) < kTinyMeanBytes) {
+    const uint64_t mean = shape_mean(arena_bytes, n, slot_bytes);
+    if (mean < kTinyMeanBytes) {
         // short frames: 8-lane rows, 8 packets per one-wave workgroup (packet-rate bound, §5g)
         launch_rows<6, 8, 8, 64, true, SF_INLINE>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
                                                   nullptr, nullptr, fa);
         return hipGetLastError();
     }
-    if (ws && n > kSubBatchAbovePackets && shape_mean(arena_bytes, n, slot_bytes) >= kSmallMeanBytes) {
+    if (mean < kSmallMeanBytes) {
+        // mixes of short and long frames (the C3 mix): 8-lane rows of 12 slots (1536 bytes per row
+        // pass, so a 1500-byte frame needs no second pass), 8 packets per wave at 6 waves/SIMD (80
+        // VGPRs). The forward's header work (decision, MAC pick, segment) then serves 8 packets per
+        // instruction instead of 4; its short waves are latency-bound and every instruction is on
+        // their path: C3 mix 0.519 -> 0.587 (round 3, profiles/r03_s1_ab_fwd_c3_rows.jsonl). The plain
+        // update keeps 16-lane rows there (8-lane rows of 12 slots: C3 0.569 vs 0.594).
+        launch_rows<12, 8, 6, 64, true, SF_INLINE>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+                                                   nullptr, nullptr, fa);
+        return hipGetLastError();
+    }
+    if (ws && n > kSubBatchAbovePackets) {
         // bursts of long frames larger than the memory-side cache: per 512K-packet sub-batch, a
         // read pass whose long-frame waves write patch records instead of segments, then
         // apply_fwd_kernel while the header lines are still cached (4M x 1500 B
@@ -1378,13 +1390,17 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
                                                            uint32_t op_all,
                                                            const uint32_t* __restrict__ caps,
                                                            uint32_t cap_all,
-                                                           uint8_t* __restrict__ status) {
+                                                           uint8_t* __restrict__ status,
+                                                           uint32_t* __restrict__ obs) {
     static_assert(R == 16 || R == 8, "16- or 8-lane rows");
     constexpr uint32_t PW = 64 / R, KR = (uint32_t)(K * R);
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
     const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
+    // the footprint sample for the next call's shape (lengths other waves are editing may be read
+    // old or new: speed only)
+    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, n, lane, obs);
     const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
     uint32_t op = op_all, cap = cap_all;
     {  // the wave's edit words / capacities: scalar loads, like the descriptors
@@ -1570,7 +1586,8 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
-                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes) {
+                       uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes,
+                       uint32_t* obs) {
     (void)di;
     if (n == 0) return hipSuccess;
     // Long frames continue in batches of 6 slots (128 VGPRs, 4 waves/SIMD); batches of 2 slots
@@ -1584,13 +1601,13 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
     const dim3 g8((n + 31u) / 32u), g16((n + 15u) / 16u);
     if (mean < kVlanWtMeanBytes)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_WT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status);
+                           desc, n, ops, op_all, caps, cap_all, status, obs);
     else if (mean < kTinyMeanBytes)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status);
+                           desc, n, ops, op_all, caps, cap_all, status, obs);
     else  // 4 rows per wave, 4 waves per workgroup
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT>), g16, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status);
+                           desc, n, ops, op_all, caps, cap_all, status, obs);
     return hipGetLastError();
 }
 

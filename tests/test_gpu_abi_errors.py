@@ -125,18 +125,18 @@ def test_contexts_on_threads_are_independent():
 
 
 def test_stream_read_reference(engine):
-    """nfcs_time_stream_read (the bench's read-stream ceiling): both forms time a read of a buffer
+    """nfcs_time_stream_read (the bench's read-stream ceiling): every form times a read of a buffer
     and write nothing into it; bad arguments are rejected."""
     L = nf.lib()
     nbytes = 64 << 20
     host = np.random.default_rng(3).integers(0, 256, size=nbytes, dtype=np.uint8)
     d = engine.alloc(nbytes).upload(host)
-    for form in (0, 1, 2):
+    for form in (0, 1, 2, 3, 4, 5):
         ms = engine.time_stream_read(d, nbytes, 3, form=form)
         assert ms > 0
     assert np.array_equal(d.download(np.uint8, nbytes), host)
     ms = ctypes.c_float()
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr + 8, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL
-    assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 3, 1, None, ctypes.byref(ms)) == EINVAL
+    assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 6, 1, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 0, 0, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, None, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL

@@ -6,6 +6,7 @@ for the update, the fused L3 forward and VLAN push/pop, checked against the orac
 import numpy as np
 import pytest
 
+import netflow_amd as nf
 import oracle
 from l3_common import random_l3_case
 from vlan_common import random_vlan_case
@@ -130,6 +131,20 @@ def test_ring_burst_adapts_without_hint(engine):
         print(f"1M x 64 B in a 4 GiB ring: first call {first * 1e3:.1f} us, adapted {adapted * 1e3:.1f} us, "
               f"with the hint {hinted * 1e3:.1f} us")
         assert adapted < 1.15 * hinted + 0.005  # ms
+        # VLAN push/pop on the same ring adapts the same way (its kernel samples too); an even
+        # number of alternating push / pop calls leaves every frame as it was
+        engine.set_slot_bytes(0)
+        push = nf.vlan_push_op(100, 3)
+        vfirst = engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 2)
+        engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 10)
+        vadapted = engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 40) / 40
+        engine.set_slot_bytes(slot)
+        engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 10)
+        vhinted = engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 40) / 40
+        assert np.array_equal(a.download(np.uint8, host.nbytes), ref)
+        print(f"VLAN push/pop: first pair {vfirst / 2 * 1e3:.1f} us per call, adapted {vadapted * 1e3:.1f} us, "
+              f"with the hint {vhinted * 1e3:.1f} us")
+        assert vadapted < 1.15 * vhinted + 0.005  # ms
     finally:
         engine.set_slot_bytes(0)
         a.free()

@@ -27,7 +27,7 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         k = os.path.join(tmp, "nfcs_kernels.hip")
         open(k, "w").write(src)
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-mllvm", "-amdgpu-kernarg-preload-count=8",
                         "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "netflow_amd", "csrc"),
                         k, os.path.join(ROOT, "netflow_amd", "csrc", "nfcs_api.hip"), "-o", out], check=True)
 
