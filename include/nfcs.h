@@ -334,6 +334,12 @@ NFCS_API int nfcs_time_l3_forward_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64
  * no occupancy cap. Total milliseconds in *ms. */
 NFCS_API int nfcs_time_stream_read(nfcs_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int form,
                                    int iters, void* stream, float* ms);
+/* The read-only floor of the checksum read pass's own access pattern: `iters` launches that read the
+ * n frames of d_desc in d_arena exactly as nfcs_update_device's read pass does (16-lane rows, 6
+ * slots, the same load policies, order and occupancy), computing and writing nothing. Total
+ * milliseconds in *ms. */
+NFCS_API int nfcs_time_frames_read(nfcs_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                                   const nfcs_desc* d_desc, uint32_t n, int iters, void* stream, float* ms);
 /* Same for nfcs_vlan_device with a uniform edit: launches alternate between op_all (even
  * iterations) and op_alt (odd), so a push / pop pair leaves every frame as it was. */
 NFCS_API int nfcs_time_vlan_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,

@@ -111,6 +111,7 @@ def _declare(L):
                                    _vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_time_stream_read": ([_vp, _vp, _u64, ctypes.c_int, ctypes.c_int, _vp, _vp], ctypes.c_int),
+        "nfcs_time_frames_read": ([_vp, _vp, _u64, _vp, _u32, ctypes.c_int, _vp, _vp], ctypes.c_int),
         "nfcs_time_flow_keys_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, ctypes.c_int, _vp,
                                         ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_time_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp,
@@ -341,6 +342,15 @@ class Engine:
         p = buf.ptr if isinstance(buf, DeviceBuffer) else int(buf)
         _check(lib().nfcs_time_stream_read(self.ctx, p, nbytes & ~15, form, iters, stream,
                                            ctypes.byref(ms)), "time_stream_read")
+        return float(ms.value)
+
+    def time_frames_read(self, arena, arena_bytes, desc, n, iters, stream=None) -> float:
+        """Total ms of `iters` reads of the batch's frames in the checksum read pass's own access
+        pattern, nothing computed or written (nfcs_time_frames_read)."""
+        ms = ctypes.c_float()
+        p = lambda b: b.ptr if isinstance(b, DeviceBuffer) else int(b)
+        _check(lib().nfcs_time_frames_read(self.ctx, p(arena), arena_bytes, p(desc), n, iters, stream,
+                                           ctypes.byref(ms)), "time_frames_read")
         return float(ms.value)
 
     def time_l3_forward_device(self, arena, arena_bytes, desc, nh, n, table, table_n, iters,

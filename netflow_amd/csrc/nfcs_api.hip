@@ -928,4 +928,19 @@ NFCS_API int nfcs_time_stream_read(nfcs_ctx* c, const uint8_t* d_buf, uint64_t b
     return NFCS_OK;
 }
 
+NFCS_API int nfcs_time_frames_read(nfcs_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
+                                   const nfcs_desc* d_desc, uint32_t n, int iters, void* stream, float* ms) {
+    if (!c || !ms || iters <= 0 || !d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
+    hipStream_t st = pick(c, stream);
+    unsigned long long* sink = reinterpret_cast<unsigned long long*>(c->d_digest);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it) NFCS_HIP(nfcs::launch_frames_read(d_arena, arena_bytes, d_desc, n, sink, st));
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
 }  // extern "C"

@@ -104,6 +104,9 @@ hipError_t launch_digest(const DevInfo& di, const uint8_t* arena, uint64_t arena
 hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsigned long long* sink,
                               hipStream_t stream);
 
+hipError_t launch_frames_read(const uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
+                              unsigned long long* sink, hipStream_t stream);
+
 // host-side synthetic layout (same spec as the device generator)
 uint32_t config_len(int config, uint64_t seed, uint64_t index);
 

@@ -1837,6 +1837,58 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsi
     return hipGetLastError();
 }
 
+// The read-only floor of the checksum read pass's own access pattern (bench `stream_ceiling`): the
+// batch's frames read exactly as update_rows_kernel reads them — 16-lane rows, 6 slots, four packets
+// per wave, 256-thread workgroups held at 6 waves/SIMD, XCD-aware order, the header slot with the
+// default policy and the rest non-temporal, jumbo frames continued in batches of 6 slots — with
+// nothing computed or written (the chunks are XOR-ed into a value stored only if it equals an
+// impossible constant). A buffer stream reads the arena contiguously; this form reads what the
+// product reads, in its order, so it bounds the product on every layout (C2's 9.5 GB arena: a
+// contiguous stream measured below the product on some boxes).
+__global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                             uint32_t nblocks, const uint8_t* __restrict__ arena,
+                                                             uint64_t arena_bytes, unsigned long long* __restrict__ sink) {
+    constexpr int K = 6, R = 16, PW = 4;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;
+    if (pw >= n) return;
+    const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
+    const uint64_t off = (uint64_t)d.off16 * 16u;
+    const bool live = pw + row < n && off + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes;
+    const uint32_t nch = live ? (d.len + 15u) >> 4 : 0u;
+    const uint4* src = (const uint4*)(arena + (live ? off : 0));
+    uint4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = rl + (uint32_t)R * k;
+        v[k] = k == 0 ? ld16<0>((c < nch) ? src + c : &g_zero16) : ld16<1>((c < nch) ? src + c : &g_zero16);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint32_t cmax = wave_max_rows<R>(nch);
+    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
+        uint4 w[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = cb + rl + (uint32_t)R * k;
+            w[k] = ld16<1>((c < nch) ? src + c : &g_zero16);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc ^= w[k].x ^ w[k].y ^ w[k].z ^ w[k].w;
+    }
+    if (acc == 0x9E3779B9u && sink) *sink = acc;
+}
+
+hipError_t launch_frames_read(const uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
+                              unsigned long long* sink, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = (n + 15u) / 16u;
+    hipLaunchKernelGGL(frames_read_kernel, dim3(grid), dim3(kBlock), kRowsLdsPad, stream, desc, n, grid, arena,
+                       arena_bytes, sink);
+    return hipGetLastError();
+}
+
 uint32_t config_len(int config, uint64_t seed, uint64_t index) { return cfg_len(config, seed, index); }
 
 // header byte override at frame offset o (o < 64), or -1

@@ -135,6 +135,15 @@ def test_stream_read_reference(engine):
         ms = engine.time_stream_read(d, nbytes, 3, form=form)
         assert ms > 0
     assert np.array_equal(d.download(np.uint8, nbytes), host)
+    # the frames-read form: the batch's frames in the read pass's pattern, nothing written
+    desc = np.zeros(4097, dtype=nf.DESC_DTYPE)
+    desc["off16"] = np.arange(4097, dtype=np.uint32) * 96
+    desc["len"] = 1500
+    desc["len"][7] = 9000  # a jumbo frame: continuation batches
+    dd = engine.alloc(desc.nbytes).upload(desc)
+    assert engine.time_frames_read(d, nbytes, dd, len(desc), 3) > 0
+    assert np.array_equal(d.download(np.uint8, nbytes), host)
+    dd.free()
     ms = ctypes.c_float()
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr + 8, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 6, 1, None, ctypes.byref(ms)) == EINVAL
