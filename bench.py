@@ -521,20 +521,9 @@ def main():
     # N > 1, weak scaling: rank 0's shard timed ALONE first (the other ranks wait at the barrier,
     # their GPUs idle), with the same steps and clock as the concurrent region below, so the line
     # carries the one-GPU rate of the very workload the N ranks scale
-    solo = None
-    if ws > 1 and scaling == "weak":
-        D.barrier()
-        if rank == 0:
-            solo_t = timed_steps(eng, step, args.steps, regen if l3 else None)
-        D.barrier()
-        solo = D.sum(frame_bytes / (solo_t / args.steps) / 1e9 if rank == 0 else 0.0)
-        regen()
-
-    # timed region: barrier + device sync on both sides, max over ranks
-    D.barrier()
-    t_rank = timed_steps(eng, step, args.steps)
-    D.barrier()
-    wall = D.max(t_rank)
+    timed = lambda pre=None: timed_steps(eng, step, args.steps, pre)
+    solo, t_rank, wall = scaling_timings(D, timed, frame_bytes, args.steps, ws > 1 and scaling == "weak",
+                                         regen if l3 else None, regen)
     t0, t1 = 0.0, t_rank
     ms_per_step = wall / args.steps * 1e3
     total_frame_bytes = D.sum(frame_bytes)
@@ -717,6 +706,27 @@ def main():
         d_arena.free()
     eng.close()
     D.close()
+
+
+def scaling_timings(D, timed, frame_bytes: float, steps: int, solo_first: bool, pre=None, after=None):
+    """The timed regions of one bench line. With solo_first (N > 1, weak scaling) rank 0 first runs
+    its own shard ALONE — the other ranks wait at the barrier, their GPUs idle — with the same steps
+    and clock as the concurrent region; `after` runs on every rank between the two (the fused
+    forward's TTL refresh). Then every rank runs its shard at once between barriers. `timed(pre)`
+    returns one rank's wall seconds for `steps` steps. Returns (rank 0's solo GB/s of frames or None,
+    this rank's concurrent seconds, the max over ranks)."""
+    solo = None
+    if solo_first:
+        D.barrier()
+        solo_t = timed(pre) if D.rank == 0 else 0.0
+        D.barrier()
+        solo = D.sum(frame_bytes / (solo_t / steps) / 1e9 if D.rank == 0 else 0.0)
+        if after is not None:
+            after()
+    D.barrier()
+    t_rank = timed()
+    D.barrier()
+    return solo, t_rank, D.max(t_rank)
 
 
 def timed_steps(eng, step, steps: int, regen=None) -> float:

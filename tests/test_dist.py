@@ -131,3 +131,51 @@ def test_gloo_group_log_stays_off_stdout():
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().splitlines() == ['{"line": 1}']
     assert "[Gloo] native write" in r.stderr and "python print" in r.stderr
+
+
+def _solo_worker(rank, ws, port, q):
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws),
+                      RANK=str(rank), LOCAL_RANK=str(rank), NFCS_DIST_BACKEND="gloo")
+    import bench
+    D = bench.Dist(*bench.dist_env())
+    log = []
+
+    def timed(pre=None):  # a rank's "steps": sleeps, stamped
+        t0 = time.time()
+        if pre is not None:
+            pre()
+        time.sleep(0.05 + 0.02 * rank)
+        log.append((t0, time.time(), pre is not None))
+        return time.time() - t0
+
+    solo, t_rank, wall = bench.scaling_timings(D, timed, 2e9, 10, True, pre=lambda: None,
+                                               after=lambda: log.append(("after", time.time())))
+    D.close()
+    q.put((rank, solo, t_rank, wall, log))
+
+
+def test_two_rank_solo_shard_then_concurrent_region():
+    """bench.py's N > 1 timing (bench.scaling_timings) over gloo, 2 ranks on CPU:
+    rank 0 times its shard ALONE first (rank 1 runs nothing until rank 0 is done), every rank gets
+    rank 0's solo rate, then both time the concurrent region; the line's wall time is the max over
+    ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_solo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, solo0, t0r, wall0, log0), (_, solo1, t1r, wall1, log1) = res
+    solo_run = [e for e in log0 if len(e) == 3 and e[2]]
+    assert len(solo_run) == 1 and not any(len(e) == 3 and e[2] for e in log1)  # only rank 0 ran solo
+    conc1 = [e for e in log1 if len(e) == 3][0]
+    assert conc1[0] >= solo_run[0][1] - 1e-3  # rank 1 started after rank 0's solo region ended
+    want = 2e9 / ((solo_run[0][1] - solo_run[0][0]) / 10) / 1e9
+    assert solo0 == solo1 and abs(solo0 - want) / want < 0.2
+    assert wall0 == wall1 == max(t0r, t1r)
+    assert any(e[0] == "after" for e in log0) and any(e[0] == "after" for e in log1)
