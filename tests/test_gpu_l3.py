@@ -194,3 +194,24 @@ def test_l3_deferred_misaligned_descriptors(engine):
     engine.sync()
     assert np.array_equal(d_st.download(np.uint8, n), rst)
     assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), arena)
+
+
+@pytest.mark.parametrize("config,n", [(3, 1 << 22), (1, 1 << 22)])
+def test_l3_full_size_digests_match_reference(engine, config, n):
+    """The bench's forward workloads at full size against the compiled reference's digests
+    (configs.json l3fwd_more): the C3 mix (4M x U{64..1500} B, 8-lane rows of 12 slots) and 4M x
+    1500 B (512K sub-batches, the record-only write pass), next hop i % 9 into the fixture's table."""
+    g = json.load(open(os.path.join(GOLD, "configs.json")))
+    want = [x for x in g["l3fwd_more"] if x["config"] == config and x["first"] == 0 and x["n"] == n]
+    assert want
+    table = np.frombuffer(bytes.fromhex(g["l3fwd_c1"]["table"]), dtype=np.uint8).copy()
+    d_arena, nbytes, d_desc, _ = engine.config_batch(config, 20250620, 0, n, 128)
+    d_tab = engine.alloc(table.nbytes).upload(table)
+    d_nh = engine.alloc(4 * n).upload((np.arange(n) % 9).astype(np.uint32))
+    try:
+        engine.l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8)
+        engine.sync()
+        assert f"{engine.digest_device(d_arena, nbytes, d_desc, n, 0):016x}" == want[0]["digest_out"]
+    finally:
+        for b in (d_arena, d_desc, d_tab, d_nh):
+            b.free()
