@@ -1612,127 +1612,124 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
 }
 
 // ---- flow-key extract + hash -----------------------------------------------
-// PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) on the first
-// 128 bytes of each frame: one 8-lane DPP row per packet (lane rl holds frame bytes
-// 16rl..16rl+15, one global_load_dwordx4). Every field the key reads lies below byte 82 (l2 18 +
-// IHL 60 + 4 port bytes), so one slot covers it. Fields reach the row by the same RowHdr
-// broadcasts and 802.1Q view as the checksum plan; the record's 16 dwords are stored by lanes
-// 0-3 (64 contiguous bytes per packet).
-//
-// The access pattern is one isolated 128-byte line per frame; MI355X serves those at ~46 G
-// lines/s at a 1536-byte stride (tools/stride_read.hip) when enough are in flight. A wave
-// therefore takes K slots of 8 packets (8K packets): lane l loads descriptor pw + l in one
-// coalesced load, each row picks its slot's descriptor with ds_bpermute, and all K header
-// lines are in flight before the first is parsed (session 2's one-slot form: 8 lines per wave,
-// 22.8 G lines/s).
+// PacketClassifier::extract_flow_key + hash_flow (packet_classifier.cpp:12-108) on the first 96
+// bytes of each frame (every field the key reads lies below byte 82: l2 18 + IHL 60 + 4 port bytes).
+// hash_flow's byte-wise XOR at shift (i % 4) * 8 is the XOR of little-endian dwords.
 static_assert(sizeof(nfcs_flow_key) == 64, "nfcs_flow_key is a 64-byte record");
 
-DEV uint32_t be32x(uint32_t le) { return __builtin_bswap32(le); }
+// A wave takes 64 packets. Their header bytes 0..95 are loaded in 8-lane rows — one coalesced
+// 128-byte line per packet, 8 packets per instruction, 8 instructions in flight — and written to
+// LDS (96 bytes per packet); then lane l parses packet l on its own, reading the fields at their
+// (802.1Q- and IHL-dependent) byte offsets from LDS, so one VALU instruction serves 64 packets and
+// no DPP broadcast is needed (round 2's form parsed in 8-lane rows: 909 VALU + 539 SALU per 32
+// packets, 0.77 against 0.82 now); the 64-byte records go back through LDS so each global store
+// writes 1 KB of consecutive records.
+DEV uint32_t lds_u8(const uint8_t* b, uint32_t o) { return b[o]; }
+DEV uint32_t lds_be16(const uint8_t* b, uint32_t o) { return ((uint32_t)b[o] << 8) | b[o + 1]; }
+DEV uint32_t lds_le32(const uint8_t* b, uint32_t o) {  // any alignment, 2-byte pieces where it can
+    if ((o & 1u) == 0) return (uint32_t)*(const uint16_t*)(b + o) | ((uint32_t)*(const uint16_t*)(b + o + 2) << 16);
+    return (uint32_t)b[o] | ((uint32_t)b[o + 1] << 8) | ((uint32_t)b[o + 2] << 16) | ((uint32_t)b[o + 3] << 24);
+}
 
-// One packet per 8-lane row: c0 = frame bytes 16rl..16rl+15 (zeros past len; len 0 when the
-// descriptor is out of bounds, which yields the all-zero record and hash of a dead packet).
-// record stores non-temporal (C1 +2% over plain; write-through measured no better)
-DEV void flow_key_row(const uint4& c0, uint32_t len, uint64_t p, uint32_t n, uint32_t rl,
-                      uint32_t rowbase4, nfcs_flow_key* __restrict__ keys,
-                      uint32_t* __restrict__ hashes) {
-    constexpr int R = 8;
-    const bool live = len != 0;
-    const RowHdr<R> h{c0, rowbase4};
+constexpr uint32_t kFkRow = 96;  // LDS bytes per packet: header bytes 0..95
+
+__global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                                 uint32_t nblocks, const uint8_t* __restrict__ arena,
+                                                                 uint64_t arena_bytes, nfcs_flow_key* __restrict__ keys,
+                                                                 uint32_t* __restrict__ hashes) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * 64 * kFkRow];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t p0 = ((uint64_t)xcd_block_n(nblocks) * kWavesPerBlock + rfl(wave)) * 64u;
+    if (p0 >= n) return;
+    uint8_t* rows = lds + wave * 64u * kFkRow;
+    // lane l: descriptor of packet p0 + l (one coalesced load); dead packets read as length 0
+    const uint64_t p = p0 + lane;
+    uint2 dl = make_uint2(0u, 0u);
+    if (p < n) dl = ((const uint2*)desc)[p];
+    const uint64_t off = (uint64_t)dl.x * 16u;
+    const bool live = p < n && off + (((uint64_t)dl.y + 15u) & ~15ull) <= arena_bytes;
+    const uint32_t len = live ? dl.y : 0u;
+    // header lines in 8-lane rows: instruction k, row r -> packet 8k + r, lane rl -> chunk rl (0..5)
+    const uint32_t rl = lane & 7u, r = lane >> 3;
+    uint4 c[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t q = 8u * k + r;
+        const uint32_t qo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)dl.x);
+        const uint32_t ql = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)len);
+        const uint4* src = (const uint4*)(arena + (uint64_t)qo * 16u);
+        c[k] = ld16<0>((rl < 6u && rl * 16u < ql) ? src + rl : &g_zero16);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+        if (rl < 6u) *(uint4*)(rows + (8u * k + r) * kFkRow + 16u * rl) = c[k];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_wave_barrier();
+    // lane l parses packet l (extract_flow_key + hash_flow, packet_classifier.cpp:12-108)
+    const uint8_t* b = rows + lane * kFkRow;
     const bool eth = len >= 14;
-    const uint32_t dw0 = h.dw(0), dw1 = h.dw(1), dw2 = h.dw(2);
-    const uint32_t e12 = h.be16(12);
+    const uint32_t m0 = eth ? *(const uint32_t*)b : 0u, m1 = eth ? *(const uint32_t*)(b + 4) : 0u;
+    const uint32_t m2 = eth ? *(const uint32_t*)(b + 8) : 0u;
+    const uint32_t e12 = lds_be16(b, 12);
     const bool tagged = e12 == 0x8100u;
     uint32_t et = eth ? e12 : 0u, vlan = 0;
     if (eth && tagged && len >= 18) {  // has_vlan / vlan_id / vlan() (packet.hpp:603-618)
-        vlan = h.be16(14) & 0x0FFFu;
-        et = h.be16(16);
+        vlan = lds_be16(b, 14) & 0x0FFFu;
+        et = lds_be16(b, 16);
     }
     const uint32_t sh = tagged ? 4u : 0u;  // l2 = 18 after a tag (ethernet(), packet.hpp:410)
-    const RowHdr<R> V{strip_tag(c0, tagged), rowbase4};  // view byte o = frame byte o + sh
     const bool v4 = et == 0x0800u, v6 = et == 0x86DDu;
-    uint32_t proto = 0, sp = 0, dp = 0, s4 = 0, d4 = 0;
+    uint32_t proto = 0, sp = 0, dp = 0, s4 = 0, d4 = 0, l4 = 0;
     uint32_t s6[4] = {0, 0, 0, 0}, d6[4] = {0, 0, 0, 0};
-    uint32_t l4 = 0;  // view offset
     bool hdr = false;
     if (v4 && 34u + sh <= len) {  // ipv4() present
-        s4 = be32x(V.dw(6) >> 16 | V.dw(7) << 16);   // view bytes 26..29
-        d4 = be32x(V.dw(7) >> 16 | V.dw(8) << 16);   // view bytes 30..33
-        proto = V.b(23);
-        l4 = 14u + (V.b(14) & 15u) * 4u;
+        s4 = __builtin_bswap32(lds_le32(b, 26u + sh));
+        d4 = __builtin_bswap32(lds_le32(b, 30u + sh));
+        proto = lds_u8(b, 23u + sh);
+        l4 = 14u + (lds_u8(b, 14u + sh) & 15u) * 4u;
         hdr = true;
     } else if (v6 && 54u + sh <= len) {  // ipv6() present
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {  // view bytes 22..37 and 38..53, as LE dwords
-            s6[j] = V.dw(5 + j) >> 16 | V.dw(6 + j) << 16;
-            d6[j] = V.dw(9 + j) >> 16 | V.dw(10 + j) << 16;
+        for (uint32_t j = 0; j < 4; ++j) {
+            s6[j] = lds_le32(b, 22u + sh + 4u * j);
+            d6[j] = lds_le32(b, 38u + sh + 4u * j);
         }
-        proto = V.b(20);
+        proto = lds_u8(b, 20u + sh);
         l4 = 54u;
         hdr = true;
     }
     // tcp() needs l4 + 19 <= len (19-byte TcpHeader), udp() l4 + 8 (packet.hpp:473-535)
     if (hdr && ((proto == 6 && l4 + sh + 19u <= len) || (proto == 17 && l4 + sh + 8u <= len))) {
-        sp = V.be16(l4);        // runtime offset: ds_bpermute
-        dp = V.be16(l4 + 2u);
+        sp = lds_be16(b, l4 + sh);
+        dp = lds_be16(b, l4 + sh + 2u);
     }
-    const uint32_t m0 = eth ? dw0 : 0u, m1 = eth ? dw1 : 0u, m2 = eth ? dw2 : 0u;
-    // hash_flow (82-108): byte i of each MAC / IPv6 address at shift (i % 4) * 8
     uint32_t hv = m0 ^ (m1 & 0xFFFFu) ^ ((m1 >> 16) | (m2 << 16)) ^ (m2 >> 16);
     hv ^= vlan ^ (et << 16);
     if (v6) hv ^= s6[0] ^ s6[1] ^ s6[2] ^ s6[3] ^ d6[0] ^ d6[1] ^ d6[2] ^ d6[3];
     else hv ^= s4 ^ d4;
     hv ^= proto ^ (sp << 16) ^ dp;
     if (!live) hv = 0;
-    if (keys && rl < 4) {
-        uint4 r;
-        if (rl == 0) {
-            r = make_uint4(hv, vlan | (et << 16), (m1 >> 16) | (m2 << 16), (m2 >> 16) | (m0 << 16));
-        } else if (rl == 1) {
-            r = make_uint4((m0 >> 16) | (m1 << 16), proto | ((v6 ? 1u : 0u) << 8) | (sp << 16), dp, 0u);
-        } else if (rl == 2) {
-            r = v6 ? make_uint4(s6[0], s6[1], s6[2], s6[3]) : make_uint4(s4, 0u, 0u, 0u);
-        } else {
-            r = v6 ? make_uint4(d6[0], d6[1], d6[2], d6[3]) : make_uint4(d4, 0u, 0u, 0u);
-        }
-        if (p < n) {
-            uint4* q = (uint4*)(keys + p) + rl;
-            __builtin_nontemporal_store(u32x4_t{r.x, r.y, r.z, r.w}, (u32x4_t*)q);
+    if (hashes && p < n) hashes[p] = hv;
+    if (!keys) return;
+    // the record (nfcs_flow_key: hash, vlan, ethertype, MACs, ports, addresses) into this lane's LDS row, then 1 KB of
+    // consecutive records per store instruction
+    uint4* rec = (uint4*)(rows + lane * kFkRow);
+    __builtin_amdgcn_wave_barrier();
+    rec[0] = make_uint4(hv, vlan | (et << 16), (m1 >> 16) | (m2 << 16), (m2 >> 16) | (m0 << 16));
+    rec[1] = make_uint4((m0 >> 16) | (m1 << 16), proto | ((v6 ? 1u : 0u) << 8) | (sp << 16), dp, 0u);
+    rec[2] = v6 ? make_uint4(s6[0], s6[1], s6[2], s6[3]) : make_uint4(s4, 0u, 0u, 0u);
+    rec[3] = v6 ? make_uint4(d6[0], d6[1], d6[2], d6[3]) : make_uint4(d4, 0u, 0u, 0u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t q = 16u * j + (lane >> 2);  // packet of this 16-byte piece
+        const uint4 v = *(const uint4*)(rows + q * kFkRow + 16u * (lane & 3u));
+        if (p0 + q < n) {
+            uint4* dst = (uint4*)(keys + p0 + q) + (lane & 3u);
+            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)dst);
         }
     }
-    if (hashes && rl == 0 && p < n) hashes[p] = hv;
-}
-
-template <int K, int BS = kBlock>
-__global__ __launch_bounds__(BS) void flow_keys_kernel(const uint8_t* __restrict__ arena,
-                                                           uint64_t arena_bytes,
-                                                           const nfcs_desc* __restrict__ desc,
-                                                           uint32_t n, nfcs_flow_key* __restrict__ keys,
-                                                           uint32_t* __restrict__ hashes) {
-    static_assert(K >= 1 && K <= 8, "slots of 8 packets per wave");
-    constexpr int R = 8;
-    constexpr uint32_t PR = 64 / R, PW = PR * K;  // rows per wave, packets per wave
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
-    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = ((uint64_t)xcd_block() * (BS / 64) + rfl(threadIdx.x >> 6)) * PW;
-    if (pw >= n) return;
-    uint2 dl = make_uint2(0u, 0u);  // lane l: descriptor of packet pw + l
-    if (lane < PW && pw + lane < n) dl = ((const uint2*)desc)[pw + lane];
-    uint4 c[K];
-    uint32_t L[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t sl = (uint32_t)k * PR + row;  // slot k, this row: packet pw + sl
-        const uint32_t off16 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.x);
-        const uint32_t dlen = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sl * 4u), (int)dl.y);
-        const uint64_t off = (uint64_t)off16 * 16u;
-        const bool live = pw + sl < n && off + (((uint64_t)dlen + 15u) & ~15ull) <= arena_bytes;
-        L[k] = live ? dlen : 0u;
-        const uint4* src = (const uint4*)(arena + (live ? off : 0));
-        c[k] = ld16<0>((rl * 16u < L[k]) ? src + rl : &g_zero16);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        flow_key_row(c[k], L[k], pw + (uint32_t)k * PR + row, n, rl, rowbase4, keys, hashes);
 }
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
@@ -1740,10 +1737,11 @@ hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t ar
                             uint32_t* hashes, hipStream_t stream) {
     (void)di;
     if (n == 0) return hipSuccess;
-    // 32 packets per wave (K = 4 slots of 8: K = 1 / 2 / 8 measured 0.59 / 0.68 / 0.67 against
-    // 0.72), non-temporal record stores (+1.5-2% over plain), XCD-aware block order (+1.5-2%)
-    hipLaunchKernelGGL((flow_keys_kernel<4>), dim3((n + 127u) / 128u),
-                       dim3(kBlock), 0, stream, arena, arena_bytes, desc, n, keys, hashes);
+    // 64 packets per wave, one lane each (round 3: C1 0.77 -> 0.82 against round 2's 8-lane rows of
+    // 4 slots; profiles/r03_s2_ab_flowkey_lanes.jsonl); non-temporal record stores, XCD-aware order
+    const uint32_t g = (n + 255u) / 256u;
+    hipLaunchKernelGGL(flow_keys_lanes_kernel, dim3(g), dim3(kBlock), 0, stream, desc, n, g, arena, arena_bytes, keys,
+                       hashes);
     return hipGetLastError();
 }
 

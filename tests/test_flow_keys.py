@@ -99,9 +99,10 @@ def test_gpu_flow_fresh_and_bad_desc(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 7, 9, 31, 33, 127, 129, 1001])
+@pytest.mark.parametrize("n", [1, 7, 9, 31, 33, 63, 65, 127, 129, 255, 257, 1001])
 def test_gpu_flow_ragged_counts(engine, n):
-    # a wave takes 32 packets (4 slots of 8 rows): counts that end mid-slot and mid-wave
+    # a wave takes 64 packets (one lane each; headers loaded 8 per instruction), a workgroup 256:
+    # counts that end mid-row, mid-wave and mid-workgroup
     frames = oracle.fuzz_frames(43, 0, n)
     arena, desc = oracle.pack_frames(frames)
     rrecs, rh = oracle.flow_keys_batch(arena, desc)
