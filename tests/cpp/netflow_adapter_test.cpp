@@ -22,11 +22,15 @@
 //         netflow_amd::update_checksums_batch (gpu), or through the single-packet CPU members of
 //         netflow_amd::Packet (cpu); the reference's per-packet calls on copies are the checker at
 //         each step. Prints "frames=N steps=2 mismatches=M expect_ne_failed=F rc=R".
+//   icmp-gpu / icmp-cpu  (no input) IcmpProcessorTest's scenarios (tests/icmp_processor_test.cpp:
+//         278-407) and the packets IcmpProcessor builds from them (icmp_processor.cpp:96-180,
+//         255-336), in two stages of update_checksums() over bursts (see icmp_mode).
 // Frames where the reference itself reads or writes outside its buffer (IHL past the frame; a push
 // without tailroom into a buffer whose capacity holds len + 4; a re-tag of a runt in a buffer of
 // fewer than 16 bytes) are skipped: there the reference is undefined.
 #include <netflow++/packet.hpp>
 
+#include <algorithm>
 #include <cstdio>
 #include <iostream>
 #include <memory>
@@ -330,6 +334,208 @@ int path_mode(bool gpu) {
     return bad || ne_failed || rc ? 1 : 0;
 }
 
+// One update_checksums() over every packet of `burst` by the engine: the GPU batch entry, or the
+// single-packet CPU members of netflow_amd::Packet on a copy of each frame. Returns the batch rc.
+int engine_update(bool gpu, std::vector<netflow::Packet*>& burst) {
+    if (gpu) return netflow_amd::update_checksums_batch(burst);
+    for (netflow::Packet* p : burst) {
+        netflow::PacketBuffer* b = p->get_buffer();
+        const size_t len = b->get_data_length();
+        netflow_amd::PacketBuffer mb(kHeadroom + len, kHeadroom, len);
+        if (len) std::memcpy(mb.get_data_start_ptr(), b->get_data_start_ptr(), len);
+        netflow_amd::Packet mp(&mb);
+        mp.update_checksums();
+        if (len) std::memcpy(b->get_data_start_ptr(), mb.get_data_start_ptr(), len);
+    }
+    return 0;
+}
+
+// The reference's sum (packet.hpp:894-912: big-endian words, an odd last byte added as the LOW
+// byte, end-around carry) over `n` bytes: a message whose checksum field holds what
+// update_checksums() wrote sums to 0xFFFF under it, odd lengths included.
+uint32_t ref_sum(const uint8_t* p, size_t n) {
+    uint32_t s = 0;
+    for (size_t i = 0; i + 1 < n; i += 2) s += (uint32_t)p[i] << 8 | p[i + 1];
+    if (n & 1) s += p[n - 1];
+    while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
+    return s;
+}
+
+void put16(std::vector<uint8_t>& d, uint16_t v) { d.push_back((uint8_t)(v >> 8)); d.push_back((uint8_t)v); }
+void put_bytes(std::vector<uint8_t>& d, const uint8_t* p, size_t n) { d.insert(d.end(), p, p + n); }
+
+// Ethernet II (IPv4) + a 20-byte IPv4 header with a zero checksum, as the ICMP test's builders
+// (icmp_processor_test.cpp:103-124, 153-174) and IcmpProcessor (icmp_processor.cpp:142-158,
+// 296-311) lay them out. Addresses are given as the four bytes in wire order.
+std::vector<uint8_t> eth_ipv4(const uint8_t* dst_mac, const uint8_t* src_mac, uint16_t id, uint8_t ttl,
+                              uint8_t proto, const uint8_t* sip, const uint8_t* dip, size_t l4_bytes) {
+    std::vector<uint8_t> d;
+    put_bytes(d, dst_mac, 6);
+    put_bytes(d, src_mac, 6);
+    put16(d, 0x0800);
+    d.push_back(0x45); d.push_back(0x00);
+    put16(d, (uint16_t)(20 + l4_bytes));
+    put16(d, id);
+    put16(d, 0x0000);
+    d.push_back(ttl); d.push_back(proto);
+    put16(d, 0x0000);
+    put_bytes(d, sip, 4);
+    put_bytes(d, dip, 4);
+    return d;
+}
+
+// IcmpProcessorTest's scenarios (tests/icmp_processor_test.cpp:278-407) on a burst of `reps`
+// repetitions (repetition 0 = the test's exact frames; later ones vary ids, sequence numbers,
+// payloads and addresses). Stage 1: the test's builders finish with update_checksums()
+// (create_icmp_echo_request_packet, 193; create_ipv4_packet_for_icmp_test, 133 — UDP whose 8-byte
+// "payload" is the UDP header, length 0xCAFE, so only the IPv4 checksum is written). Stage 2: from
+// the ENGINE's stage-1 packets, the packets IcmpProcessor builds — the echo reply
+// (send_icmp_echo_reply, icmp_processor.cpp:96-180) and the Time Exceeded / Destination
+// Unreachable messages (send_icmp_error_packet_base, 255-336; the random IP id is made
+// deterministic) — then update_checksums() (180, 336). At both stages the reference's per-packet
+// calls on copies are the checker; then the test's EXPECTs on the reply (313-338), and on every
+// packet: IPv4 header and ICMP message sum to 0xFFFF under the reference's own sum.
+// Prints "frames=N stages=2 mismatches=M expect_failed=F rc=R".
+int icmp_mode(bool gpu) {
+    const size_t reps = gpu ? 1024 : 4;
+    const uint8_t my_mac[6] = {0x00, 0xAA, 0xBB, 0xCC, 0xDD, 0xEE};
+    const uint8_t req_mac[6] = {0x11, 0x22, 0x33, 0x44, 0x55, 0x66};
+    const uint8_t my_ip[4] = {192, 168, 0, 1};
+    const uint8_t orig_src_mac[6] = {0xDE, 0xAD, 0xBE, 0xEF, 0x00, 0x01};
+    const uint8_t orig_dst_mac[6] = {0xDE, 0xAD, 0xBE, 0xEF, 0x00, 0x02};
+    const uint8_t orig_src_ip[4] = {192, 168, 1, 100};
+    const uint8_t te_dst_ip[4] = {172, 16, 1, 100};
+    const uint8_t nu_dst_ip[4] = {203, 0, 113, 5};
+    const uint8_t err_src_mac[6] = {0x0A, 0x00, 0x00, 0x00, 0x00, 0x01};
+    const uint8_t nh_mac[6] = {0x0A, 0x00, 0x00, 0x00, 0x00, 0x02};
+    const uint8_t err_src_ip[4] = {10, 0, 0, 1};
+    const uint8_t l4_payload[8] = {0xDE, 0xAD, 0xBE, 0xEF, 0xCA, 0xFE, 0xBA, 0xBE};
+
+    struct Req { uint16_t id, seq; std::vector<uint8_t> payload; uint8_t req_ip[4]; };
+    std::vector<Req> reqs(reps);
+    std::vector<std::vector<uint8_t>> s1;  // per repetition: echo request, TE original, NU original
+    for (size_t r = 0; r < reps; ++r) {
+        Req& q = reqs[r];
+        q.id = (uint16_t)(1234 + r);
+        q.seq = (uint16_t)(1 + r);
+        q.payload = {'h', 'e', 'l', 'l', 'o'};
+        for (size_t i = 0; i < r % 64; ++i) q.payload.push_back((uint8_t)(r * 31 + i));  // odd and even sizes
+        const uint8_t rip[4] = {192, 168, 0, (uint8_t)(100 + r % 100)};
+        std::memcpy(q.req_ip, rip, 4);
+        std::vector<uint8_t> e = eth_ipv4(my_mac, req_mac, 54321, 64, 1, q.req_ip, my_ip, 8 + q.payload.size());
+        e.push_back(8); e.push_back(0);  // TYPE_ECHO_REQUEST, code 0
+        put16(e, 0x0000);
+        put16(e, q.id);
+        put16(e, q.seq);
+        put_bytes(e, q.payload.data(), q.payload.size());
+        std::vector<uint8_t> te = eth_ipv4(orig_dst_mac, orig_src_mac, 12345, 1, 17, orig_src_ip, te_dst_ip, 8);
+        put_bytes(te, l4_payload, 8);
+        std::vector<uint8_t> nu = eth_ipv4(orig_dst_mac, orig_src_mac, 12345, 64, 17, orig_src_ip, nu_dst_ip, 8);
+        put_bytes(nu, l4_payload, 8);
+        s1.push_back(e); s1.push_back(te); s1.push_back(nu);
+    }
+
+    int rc = 0;
+    size_t bad = 0, failed = 0, frames = 0;
+    // one stage: buffers for the engine and the reference, the engine's burst, the reference's calls
+    auto stage = [&](const std::vector<std::vector<uint8_t>>& fs, std::vector<std::unique_ptr<netflow::PacketBuffer>>& gb,
+                     std::vector<std::unique_ptr<netflow::Packet>>& gp) {
+        std::vector<std::unique_ptr<netflow::PacketBuffer>> rb;
+        std::vector<std::unique_ptr<netflow::Packet>> rp;
+        std::vector<netflow::Packet*> burst;
+        for (const auto& f : fs) {
+            gb.push_back(ref_buffer(f, f.size()));
+            rb.push_back(ref_buffer(f, f.size()));
+            gp.emplace_back(new netflow::Packet(gb.back().get()));
+            rp.emplace_back(new netflow::Packet(rb.back().get()));
+            burst.push_back(gp.back().get());
+        }
+        const int r = engine_update(gpu, burst);
+        if (r) rc = r;
+        for (size_t i = 0; i < fs.size(); ++i) {
+            rp[i]->update_checksums();
+            bad += std::memcmp(gb[i]->get_data_start_ptr(), rb[i]->get_data_start_ptr(), fs[i].size()) != 0;
+            const uint8_t* f = gb[i]->get_data_start_ptr();
+            failed += ref_sum(f + 14, 20) != 0xFFFFu;                                   // IPv4 header
+            if (f[23] == 1) failed += ref_sum(f + 34, fs[i].size() - 34) != 0xFFFFu;    // ICMP message
+        }
+        frames += fs.size();
+    };
+    std::vector<std::unique_ptr<netflow::PacketBuffer>> b1, b2;
+    std::vector<std::unique_ptr<netflow::Packet>> p1, p2;
+    stage(s1, b1, p1);
+
+    std::vector<std::vector<uint8_t>> s2;  // per repetition: echo reply, Time Exceeded, Unreachable
+    for (size_t r = 0; r < reps; ++r) {
+        // the echo reply from the engine's request (icmp_processor.cpp:96-173)
+        const netflow::Packet& rq = *p1[3 * r];
+        const netflow::IPv4Header* ip = rq.ipv4();
+        const netflow::IcmpHeader* ic = rq.icmp();
+        if (!ip || !ic) { ++failed; continue; }
+        const uint8_t* q = rq.get_buffer()->get_data_start_ptr();
+        const size_t ihl = (size_t)(q[14] & 15u) * 4u;
+        size_t pay = ntohs(ip->total_length) - ihl - 8;
+        const size_t pay_off = 14 + ihl + 8;
+        if (pay_off + pay > rq.get_buffer()->get_data_length()) pay = 0;
+        std::vector<uint8_t> e = eth_ipv4(q + 6, my_mac, 0, 64, 1, q + 14 + 16, q + 14 + 12, 8 + pay);
+        e.push_back(0); e.push_back(0);  // TYPE_ECHO_REPLY, code 0
+        put16(e, 0x0000);
+        put_bytes(e, q + 14 + ihl + 4, 4);  // identifier and sequence number as they were
+        put_bytes(e, q + pay_off, pay);
+        s2.push_back(e);
+        // Time Exceeded (11/0) and Destination Unreachable (3/0) from the engine's originals
+        // (icmp_processor.cpp:255-327): the original IPv4 header and up to 8 bytes after it
+        for (int k = 0; k < 2; ++k) {
+            const netflow::Packet& o = *p1[3 * r + 1 + k];
+            const uint8_t* g = o.get_buffer()->get_data_start_ptr();
+            const size_t olen = o.get_buffer()->get_data_length();
+            const size_t oihl = (size_t)(g[14] & 15u) * 4u;
+            const size_t l4 = std::min<size_t>(8, olen > 14 + oihl ? olen - 14 - oihl : 0);
+            std::vector<uint8_t> m = eth_ipv4(nh_mac, err_src_mac, (uint16_t)(0x1234 + 2 * r + k), 64, 1, err_src_ip,
+                                              g + 14 + 12, 8 + oihl + l4);
+            m.push_back(k == 0 ? 11 : 3); m.push_back(0);
+            put16(m, 0x0000);
+            put16(m, 0x0000);
+            put16(m, 0x0000);
+            put_bytes(m, g + 14, oihl + l4);
+            s2.push_back(m);
+        }
+    }
+    stage(s2, b2, p2);
+
+    // ReceiveEchoRequestAndSendReply's EXPECTs (icmp_processor_test.cpp:313-338) on the engine's reply
+    for (size_t r = 0; r < reps && 3 * r < p2.size(); ++r) {
+        const netflow::Packet& rp = *p2[3 * r];
+        const netflow::EthernetHeader* eh = rp.ethernet();
+        const netflow::IPv4Header* ih = rp.ipv4();
+        const netflow::IcmpHeader* ch = rp.icmp();
+        if (!eh || !ih || !ch) { ++failed; continue; }
+        netflow::IpAddress mine, theirs;
+        std::memcpy(&mine, my_ip, 4);
+        std::memcpy(&theirs, reqs[r].req_ip, 4);
+        failed += !(eh->dst_mac == netflow::MacAddress(req_mac));
+        failed += !(eh->src_mac == netflow::MacAddress(my_mac));
+        failed += ntohs(eh->ethertype) != netflow::ETHERTYPE_IPV4;
+        failed += ih->src_ip != mine || ih->dst_ip != theirs || ih->protocol != netflow::IPPROTO_ICMP;
+        failed += ch->type != netflow::IcmpHeader::TYPE_ECHO_REPLY || ch->code != 0;
+        failed += ntohs(ch->identifier) != reqs[r].id || ntohs(ch->sequence_number) != reqs[r].seq;
+        const size_t po = 14 + 20 + 8;
+        const std::vector<uint8_t>& pl = reqs[r].payload;
+        failed += rp.get_buffer()->get_data_length() < po + pl.size() ||
+                  std::memcmp(rp.get_buffer()->get_data_start_ptr() + po, pl.data(), pl.size()) != 0;
+        // the error messages carry type/code and the original header + 8 bytes
+        for (int k = 0; k < 2; ++k) {
+            const netflow::Packet& m = *p2[3 * r + 1 + k];
+            const uint8_t* g = m.get_buffer()->get_data_start_ptr();
+            const uint8_t* o = p1[3 * r + 1 + k]->get_buffer()->get_data_start_ptr();
+            failed += g[34] != (k == 0 ? 11 : 3) || g[35] != 0;
+            failed += m.get_buffer()->get_data_length() != 14 + 20 + 8 + 28 || std::memcmp(g + 42, o + 14, 28) != 0;
+        }
+    }
+    std::printf("frames=%zu stages=2 mismatches=%zu expect_failed=%zu rc=%d\n", frames, bad, failed, rc);
+    return bad || failed || rc ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -340,6 +546,8 @@ int main(int argc, char** argv) {
     if (mode == "vgpu") return vgpu_mode();
     if (mode == "path-gpu") return path_mode(true);
     if (mode == "path-cpu") return path_mode(false);
+    if (mode == "icmp-gpu") return icmp_mode(true);
+    if (mode == "icmp-cpu") return icmp_mode(false);
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 2;
 }

@@ -123,3 +123,27 @@ def test_reference_path_scenario_gpu_burst(exe):
     r, kv = _path_scenario(exe, "path-gpu")
     assert r.returncode == 0, r.stdout + r.stderr
     assert kv == {"frames": 3072, "steps": 2, "mismatches": 0, "expect_ne_failed": 0, "rc": 0}
+
+
+def test_reference_icmp_scenarios_cpu(exe):
+    """IcmpProcessorTest (tests/icmp_processor_test.cpp:278-407): the test's echo request and UDP
+    originals (its builders end in update_checksums(), 133 / 193), then the echo reply and the Time
+    Exceeded / Destination Unreachable messages IcmpProcessor builds from them
+    (icmp_processor.cpp:96-180, 255-336) and checksums (180, 336) — through netflow_amd::Packet's
+    single-packet CPU members, 4 repetitions (the first is the test's exact frames). Bytes equal the
+    reference's per-packet results at both stages; the test's EXPECTs on the reply hold; every IPv4
+    header and ICMP message sums to 0xFFFF under the reference's own sum (odd lengths included)."""
+    r, kv = _path_scenario(exe, "icmp-cpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv == {"frames": 24, "stages": 2, "mismatches": 0, "expect_failed": 0, "rc": 0}
+
+
+@pytest.mark.gpu
+def test_reference_icmp_scenarios_gpu_burst(exe):
+    """The same two stages as bursts of 3072 netflow::Packet each (1024 repetitions: ICMP payloads of
+    5-68 bytes, odd and even; varying ids, sequence numbers and requester addresses) through
+    netflow_amd::update_checksums_batch on the GPU; the replies and error messages are built from the
+    ENGINE's stage-1 packets."""
+    r, kv = _path_scenario(exe, "icmp-gpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert kv == {"frames": 6144, "stages": 2, "mismatches": 0, "expect_failed": 0, "rc": 0}
