@@ -25,20 +25,44 @@ namespace cpu {
 
 inline uint32_t be16(const unsigned char* f, size_t o) { return (uint32_t(f[o]) << 8) | f[o + 1]; }
 
-// calculate_checksum's running sum (packet.hpp:898-905): big-endian 16-bit words, and an odd
-// trailing byte added as the LOW byte of a word (the reference's quirk, not RFC 1071's high byte).
-inline uint32_t word_sum(const unsigned char* p, size_t n) {
-    uint32_t s = 0;
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "the sums below read little-endian words");
+
+// calculate_checksum's running sum (packet.hpp:898-905) in the little-endian domain: the reference adds big-endian 16-bit words and an odd trailing byte as the LOW byte of a
+// word (its quirk, not RFC 1071's high byte). One's-complement addition commutes with the byte swap
+// (RFC 1071 §2(B)), so the sum of the region's little-endian 16-bit words — zero exactly when every
+// byte is — folds to the byte swap of the reference's fold (finish below); the odd byte b, a big-endian value b, is b << 8 here.
+// (The GPU kernels use the same identity)
+
+// Lanes of four 32-bit words (GCC/Clang vector extension: SSE2 / NEON code at -O2, no intrinsics).
+typedef uint32_t le_v4 __attribute__((vector_size(16)));
+
+inline uint64_t le_sum(const unsigned char* p, size_t n) {
+    // 16 bytes per step: the low and the high 16-bit words of four dwords added into separate 32-bit
+    // lanes; a lane adds at most 0xFFFF per step, so it cannot wrap for regions below 1 MiB (the
+    // callers' regions are below 2^16 + 60 bytes)
+    le_v4 lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
     size_t i = 0;
-    for (; i + 1 < n; i += 2) s += be16(p, i);
-    if (n & 1) s += p[n - 1];
+    for (; i + 16 <= n; i += 16) {
+        le_v4 v;
+        std::memcpy(&v, p + i, 16);
+        lo += v & 0xFFFFu;
+        hi += v >> 16;
+    }
+    uint64_t s = 0;
+    for (int k = 0; k < 4; ++k) s += (uint64_t)lo[k] + hi[k];
+    for (; i + 1 < n; i += 2) s += uint32_t(p[i]) | (uint32_t(p[i + 1]) << 8);
+    if (n & 1) s += uint32_t(p[n - 1]) << 8;
     return s;
 }
 
-// End-around carry, complement (packet.hpp:907-911): the value the reference stores big-endian.
-inline uint32_t finish(uint32_t s) {
+// A big-endian-domain 16-bit term (the pseudo-header's protocol and length) in the little-endian domain.
+inline uint64_t le_term(uint32_t be) { return ((be & 0xFFu) << 8) | ((be >> 8) & 0xFFu); }
+
+// End-around carry, complement (packet.hpp:907-911) of a little-endian-domain sum: the value the
+// reference stores big-endian. A zero sum gives 0xFFFF, any other multiple of 0xFFFF 0x0000, as there.
+inline uint32_t finish(uint64_t s) {
     while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
-    return ~s & 0xFFFFu;
+    return ~(((s & 0xFFu) << 8) | (s >> 8)) & 0xFFFFu;
 }
 
 inline void put_be16(unsigned char* f, size_t o, uint32_t v) {
@@ -63,7 +87,7 @@ inline uint8_t update_checksums(unsigned char* f, size_t len) noexcept {
         l4 = l2 + ihl4;
         if (l4 > len) return NFCS_ST_OOB;
         f[l2 + 10] = f[l2 + 11] = 0;
-        put_be16(f, l2 + 10, finish(word_sum(f + l2, ihl4)));
+        put_be16(f, l2 + 10, finish(le_sum(f + l2, ihl4)));
         st = NFCS_ST_V4;
     } else {
         uint32_t et = len >= 14 ? be16(f, 12) : 0u;
@@ -109,11 +133,10 @@ inline uint8_t update_checksums(unsigned char* f, size_t len) noexcept {
         return st;
     }
     f[field] = f[field + 1] = 0;           // zeroed, then the pseudo-header and the segment read
-    uint32_t s = 0;
-    if (proto != 1)
-        s = v4 ? word_sum(f + l2 + 12, 8) + proto + seg
-               : word_sum(f + l2 + 8, 32) + (seg >> 16) + (seg & 0xFFFFu) + proto;
-    s += word_sum(f + l4, seg);
+    uint64_t s = 0;
+    if (proto != 1)  // {src, dst, 0, proto, seg} (IPv6: {src16, dst16, seg32, 0, 0, 0, nh}); seg < 2^16
+        s = le_sum(f + l2 + (v4 ? 12 : 8), v4 ? 8 : 32) + le_term(proto) + le_term(seg);
+    s += le_sum(f + l4, seg);
     uint32_t c = finish(s);
     if (proto == 17 && c == 0) c = 0xFFFFu;  // UDP only (packet.hpp:867-871)
     put_be16(f, field, c);

@@ -31,6 +31,7 @@
 #include <netflow++/packet.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <iostream>
 #include <memory>
@@ -536,10 +537,58 @@ int icmp_mode(bool gpu) {
     return bad || failed || rc ? 1 : 0;
 }
 
+// The single-packet CPU path against the reference's on one core: `n` IPv4/UDP frames of `len` bytes
+// (random payload, stale checksums), each updated in place `reps` times by the reference's
+// Packet::update_checksums() and by netflow_amd::Packet::update_checksums() (cpu_update.hpp), the
+// two interleaved per pass so both see the same cache state; then the two arenas compared.
+// Prints "frames=N len=L ref_ns=… engine_ns=… speedup=… mismatches=M" (ns per packet).
+int cpubench_mode(size_t len, size_t n, size_t reps) {
+    if (len < 42) len = 42;
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return (uint8_t)x; };
+    std::vector<std::unique_ptr<netflow::PacketBuffer>> rb;
+    std::vector<std::unique_ptr<netflow::Packet>> rp;
+    std::vector<std::unique_ptr<netflow_amd::PacketBuffer>> mb;
+    std::vector<std::unique_ptr<netflow_amd::Packet>> mp;
+    for (size_t i = 0; i < n; ++i) {
+        std::vector<uint8_t> f(len);
+        for (auto& b : f) b = rnd();
+        f[12] = 0x08; f[13] = 0x00; f[14] = 0x45; f[15] = 0;
+        f[16] = (uint8_t)((len - 14) >> 8); f[17] = (uint8_t)(len - 14);
+        f[22] = 64; f[23] = 17;
+        f[38] = (uint8_t)((len - 34) >> 8); f[39] = (uint8_t)(len - 34);
+        rb.push_back(ref_buffer(f, len));
+        rp.emplace_back(new netflow::Packet(rb.back().get()));
+        mb.emplace_back(new netflow_amd::PacketBuffer(kHeadroom + len, kHeadroom, len));
+        std::memcpy(mb.back()->get_data_start_ptr(), f.data(), len);
+        mp.emplace_back(new netflow_amd::Packet(mb.back().get()));
+    }
+    double t_ref = 0, t_eng = 0;
+    for (size_t r = 0; r < reps; ++r) {
+        auto t0 = std::chrono::steady_clock::now();
+        for (size_t i = 0; i < n; ++i) rp[i]->update_checksums();
+        auto t1 = std::chrono::steady_clock::now();
+        for (size_t i = 0; i < n; ++i) mp[i]->update_checksums();
+        auto t2 = std::chrono::steady_clock::now();
+        t_ref += std::chrono::duration<double>(t1 - t0).count();
+        t_eng += std::chrono::duration<double>(t2 - t1).count();
+    }
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i)
+        bad += std::memcmp(rb[i]->get_data_start_ptr(), mb[i]->get_data_start_ptr(), len) != 0;
+    const double k = 1e9 / (double)(n * reps);
+    std::printf("frames=%zu len=%zu ref_ns=%.1f engine_ns=%.1f speedup=%.2f mismatches=%zu\n", n, len, t_ref * k,
+                t_eng * k, t_ref / t_eng, bad);
+    return bad ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (mode == "cpubench")
+        return cpubench_mode(argc > 2 ? std::stoul(argv[2]) : 1500, argc > 3 ? std::stoul(argv[3]) : 4096,
+                             argc > 4 ? std::stoul(argv[4]) : 50);
     if (mode == "cpu") return cpu_mode();
     if (mode == "vcpu") return vcpu_mode();
     if (mode == "gpu") return gpu_mode();
