@@ -596,6 +596,7 @@ struct RowStage {
     uint32_t p;
     uint32_t valid, bad;
     uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
+    uint32_t mis;   // 16-byte chunks between the frame start and the 128-byte line below it
 };
 
 // Per-launch extras of update_rows_kernel: the fused L3 forward's inputs (unused by the plain
@@ -627,8 +628,14 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
 // (evict-first). Every load is always issued — lanes past the frame read g_zero16 — so the waits
-// are counted vmcnt waits.
-template <int K, int R = 16, bool FWD = false>
+// are counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
+// R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
+// each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
+// frame's alignment; lanes before the frame start or past its end read g_zero16. Frame-relative
+// windows on a frame that starts mid-line make every instruction touch one line more (densely
+// packed frames: C1 -4.5%, C2 -8%, C3 -15%; 64-byte-aligned starts C1 -5%;
+// profiles/r03_s3_ab_align*.jsonl). Without LA, mis = 0 and the windows are frame-relative.
+template <int K, int R = 16, bool FWD = false, bool LA = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
                    uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0) {
     const bool valid = p64 < n;
@@ -641,12 +648,13 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     S.p = (uint32_t)p64;
     S.len = live ? d.len : 0u;
     S.frame = arena + (live ? off : 0);
+    S.mis = LA && live ? (uint32_t)(((uintptr_t)S.frame >> 4) & 7u) : 0u;
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t c = rl + (uint32_t)R * k;
+        const uint32_t c = rl + (uint32_t)R * k - S.mis;  // frame chunk (wraps below the frame start)
         const uint4* a = (c < nch) ? src + c : &g_zero16;
         S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
     }
@@ -687,7 +695,25 @@ DEV uint2 fwd_record(uint32_t ipw, uint32_t l4w, uint32_t ttl_new, uint32_t prot
 DEV bool defer_group(uint32_t lensum, uint32_t P) { return lensum >= P * (uint32_t)kDeferMeanBytes; }
 DEV uint32_t defer_len(uint32_t len) { return len < 0xFFFFu ? len : 0xFFFFu; }
 
-template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false>
+// Frame chunk rl (rl < R) of the row's packet from its line-aligned slots 0 and 1: the header
+// view the plan, the forward's rewrite and its segment stores work on (lane rl + mis of the row).
+template <int K, int R>
+DEV uint4 hdr_view(const RowStage<K>& S, uint32_t rowbase4, uint32_t rl) {
+    const uint32_t a = rl + S.mis;
+    const int sl = (int)(rowbase4 + (a & (R - 1)) * 4u);
+    const uint4 v0 = S.v[0], v1 = S.v[1];
+    const uint4 r0 = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v0.x),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v0.y),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v0.z),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v0.w));
+    const uint4 r1 = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v1.x),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v1.y),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v1.z),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v1.w));
+    return a < (uint32_t)R ? r0 : r1;
+}
+
+template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false>
 DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
                      const uint32_t* wmac = nullptr, const nfcs_nexthop* table = nullptr) {
@@ -695,7 +721,10 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     uint8_t* frame = S.frame;
     const uint4* src = (const uint4*)frame;
     const bool live = S.valid && !S.bad;
+    static_assert(K >= 2, "the header view reads slots 0 and 1");
+    // frame chunk rl in lane rl: slot 0 itself when every row of the wave starts on a line
     uint4 h0 = S.v[0];
+    if (LA && __builtin_amdgcn_ballot_w64(S.mis != 0) != 0) h0 = hdr_view<K, R>(S, rowbase4, rl);
     // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
     // rewrite applied to the header registers, so the checksums below see the new header.
     bool fwd = false, tagged = false;
@@ -743,9 +772,12 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     const uint32_t ipw = (P.flags & F_IP) ? P.ipw : NFCS_PATCH_NONE;
     uint32_t l4w = NFCS_PATCH_NONE;
     // Region sums without per-slot boundary branches (rows without an L4 region add nothing):
-    // chunks below nre are added whole (the region starts below byte 80, in slot 0, where
-    // dwords under lo4 are masked); the last chunk's bytes past re and the odd trailing byte
-    // are corrected once per row by the lane that holds it. Frames longer than one batch leave
+    // chunks below nre are added whole (the region starts below byte 80, in the header view h0,
+    // where dwords under lo4 are masked); the last chunk's bytes past re and the odd trailing byte
+    // are corrected once per row by the lane that holds it. The header view stands for slot 0:
+    // it holds frame chunks 0..R-1 in lanes 0..R-1, so slot 0's own lanes (frame chunks below
+    // R - mis) are never summed and slot 1 adds only its chunks from R on; lane rl of slot k >= 1
+    // holds frame chunk R*k + rl - mis (row_stage). Frames longer than one batch leave
     // their end to the masked continuation below. rlv is opaque so the per-slot offsets are
     // recomputed rather than hoisted into ~35 long-lived VGPRs.
     const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
@@ -755,13 +787,15 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     uint32_t acc = 0;
     const uint32_t nre = (re + 15u) >> 4;
     {
-        const uint32_t last = nre - 1u, own = (re != 0) && (last < (uint32_t)R * K) && ((last & (R - 1)) == rl);
+        // la: the last chunk's place in the slots (lane la % R of slot la / R; slot 0 = h0)
+        const uint32_t last = nre - 1u, la = (!LA || last < (uint32_t)R) ? last : last + S.mis;
+        const uint32_t own = (re != 0) && (la < (uint32_t)R * K) && ((la & (R - 1)) == rl);
         uint4 lc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint4 v = k == 0 ? h0 : S.v[k];
-            const uint32_t c = rlv + (uint32_t)R * k;
-            const uint32_t m = (c < nre) ? 0xFFFFFFFFu : 0u;
+            const uint32_t c = k == 0 ? rlv : rlv + (uint32_t)R * k - S.mis;
+            const uint32_t m = (c < nre && (!LA || k != 1 || c >= (uint32_t)R)) ? 0xFFFFFFFFu : 0u;
             if (k == 0) {
                 const uint32_t o = 16u * c;
                 acc = wsum(v.x & m & ((o >= lo4) ? 0xFFFFFFFFu : 0u), acc);
@@ -771,7 +805,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             } else {
                 acc = wsum(v.w & m, wsum(v.z & m, wsum(v.y & m, wsum(v.x & m, acc))));
             }
-            const bool sel = (last >> (R == 16 ? 4 : 3)) == (uint32_t)k;
+            const bool sel = (la >> (R == 16 ? 4 : 3)) == (uint32_t)k;
             lc.x = sel ? v.x : lc.x;
             lc.y = sel ? v.y : lc.y;
             lc.z = sel ? v.z : lc.z;
@@ -794,16 +828,16 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         }
     }
     // continuation batches for frames longer than R*K chunks (jumbo)
-    const uint32_t cmax = wave_max_rows<R>(nre);
+    const uint32_t cmax = wave_max_rows<R>(LA ? nre + S.mis : nre);
     for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
         uint4 w[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t c = cb + rlv + (uint32_t)R * k;
+            const uint32_t c = cb + rlv + (uint32_t)R * k - S.mis;
             w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k, lo4, re, tailfix);
+        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
     }
     const uint32_t z = row_sum<R>(acc) + P.corr;
     if (P.flags & F_L4) {
@@ -946,7 +980,43 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 // (-amdgpu-kernarg-preload-count=8, netflow_amd/__init__.py), so a wave's first memory access is
 // its descriptor load, with no kernel-argument round trip ahead of it; `nblocks` (= gridDim.x) is
 // passed explicitly for the same reason (the grid size is a hidden argument, loaded from memory).
-template <int K, int R, int OCC, int BS, bool FWD, int SF>
+// The rows of one wave from their frame loads on: line-aligned windows of KL slots (LA) or
+// frame-relative ones of K slots.
+template <int K, int R, int BS, bool FWD, int SF, bool LA, int PW>
+DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, uint64_t arena_bytes, uint32_t base16,
+                   uint32_t rl, uint32_t row, uint32_t rowbase4, bool defer, const uint32_t (&q)[PW],
+                   uint8_t* status, nfcs_patch* patch, nfcs_patch* ws, const nfcs_nexthop* table, uint32_t table_n) {
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
+    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
+    RowStage<K> S;
+    row_stage<K, R, FWD, LA>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, 0u);
+    uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
+    if (FWD) {
+#pragma unroll
+        for (uint32_t i = 0; i < PW; ++i) S.nh |= (row == i) ? q[i] : 0u;
+        // a deferring wave's MACs are written by apply_fwd_kernel (the checksums do not cover
+        // them): only waves that store inline load them
+        if (!(SF == SF_DEFER && defer)) {
+#pragma unroll
+            for (uint32_t i = 0; i < PW; ++i) {
+                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)&g_zero16;
+                wmac[3 * i] = m[0];
+                wmac[3 * i + 1] = m[1];
+                wmac[3 * i + 2] = m[2];
+            }
+        }
+    }
+    // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
+    // workgroups), write-through elsewhere (see row_process)
+    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER, LA>(S, rl, rowbase4, status, rec,
+                                                                                 frame_stores, table_n, wmac, table);
+}
+
+// LAM: 0 frame-relative windows of K slots; 1 line-aligned windows of KL slots; 2 per wave, line-
+// aligned (KL slots) when a row of the wave starts mid-line, else frame-relative (K slots), so
+// line-aligned batches run the frame-relative code unchanged.
+template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM, int KL>
 __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
                                                               uint32_t nblocks, uint8_t* __restrict__ arena,
                                                               uint64_t arena_bytes, uint32_t base16,
@@ -996,30 +1066,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* _
             for (uint32_t i = 0; i < PW; ++i) q[i] = (pw + i < n) ? nhp[i] : NFCS_NH_NONE;
         }
     }
-    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
-    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
-    RowStage<K> S;
-    row_stage<K, R, FWD>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, 0u);
-    uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
-    if (FWD) {
-#pragma unroll
-        for (uint32_t i = 0; i < PW; ++i) S.nh |= (row == i) ? q[i] : 0u;
-        // a deferring wave's MACs are written by apply_fwd_kernel (the checksums do not cover
-        // them): only waves that store inline load them
-        if (!(SF == SF_DEFER && defer)) {
-#pragma unroll
-            for (uint32_t i = 0; i < PW; ++i) {
-                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)&g_zero16;
-                wmac[3 * i] = m[0];
-                wmac[3 * i + 1] = m[1];
-                wmac[3 * i + 2] = m[2];
-            }
-        }
+    bool la = LAM == 1;
+    if (LAM == 2) {  // any row of the wave starting mid-line (its frame address, as row_stage computes it)
+        const nfcs_desc d = pick_desc<PW>(D, row);
+        const uint64_t a = (uint64_t)(uintptr_t)arena + ((uint64_t)d.off16 - base16) * 16u;
+        la = __builtin_amdgcn_ballot_w64(pw + row < n && d.len != 0 && ((a >> 4) & 7u) != 0) != 0;
     }
-    // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
-    // workgroups), write-through elsewhere (see row_process)
-    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER>(S, rl, rowbase4, status, rec, frame_stores,
-                                                         table_n, wmac, table);
+    if (la)
+        rows_body<KL, R, BS, FWD, SF, true, PW>(D, pw, n, arena, arena_bytes, base16, rl, row, rowbase4, defer, q,
+                                                status, patch, ws, table, table_n);
+    else
+        rows_body<K, R, BS, FWD, SF, false, PW>(D, pw, n, arena, arena_bytes, base16, rl, row, rowbase4, defer, q,
+                                                status, patch, ws, table, table_n);
 }
 
 // SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
@@ -1164,11 +1222,11 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
 enum : int { kShapeTiny = 0, kShapeShort = 1, kShapeLong = 2 };
 
 // One launch of update_rows_kernel (the grid size passed as `nblocks` too).
-template <int K, int R, int OCC, int BS, bool FWD, int SF>
+template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM = 0, int KL = K>
 static void launch_rows(uint32_t grid, unsigned lds, hipStream_t stream, uint8_t* arena, uint64_t arena_bytes,
                         const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status, nfcs_patch* patch,
                         nfcs_patch* ws, const FwdArgs& fa) {
-    hipLaunchKernelGGL((update_rows_kernel<K, R, OCC, BS, FWD, SF>), dim3(grid), dim3(BS), lds, stream, desc, n, grid,
+    hipLaunchKernelGGL((update_rows_kernel<K, R, OCC, BS, FWD, SF, LAM, KL>), dim3(grid), dim3(BS), lds, stream, desc, n, grid,
                        arena, arena_bytes, base16, fa.nh, fa.obs, status, patch, ws, fa.table, fa.table_n);
 }
 
@@ -1183,7 +1241,8 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
     const uint32_t g8 = (n + 7u) / 8u, g1 = (n + 3u) / 4u, g4 = (n + 15u) / 16u;
 #define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
-    launch_rows<6, 16, OCC, BS, false, SF>(G, BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc, \
+    launch_rows<6, 16, OCC, BS, false, SF, BS == kBlock ? 1 : 0, BS == kBlock ? 7 : 6>(                          \
+        G, BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc,                                 \
                                            n, base16, status, patch, ws, nofwd)
 #define NFCS_ROWS8(SF) \
     launch_rows<6, 8, 8, 64, false, SF>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd)
@@ -1268,7 +1327,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // instruction instead of 4; its short waves are latency-bound and every instruction is on
         // their path: C3 mix 0.519 -> 0.587 (round 3, profiles/r03_s1_ab_fwd_c3_rows.jsonl). The plain
         // update keeps 16-lane rows there (8-lane rows of 12 slots: C3 0.569 vs 0.594).
-        launch_rows<12, 8, 6, 64, true, SF_INLINE>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+        launch_rows<12, 8, 6, 64, true, SF_INLINE, 1, 12>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
                                                    nullptr, nullptr, fa);
         return hipGetLastError();
     }
@@ -1281,7 +1340,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
             const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};
-            launch_rows<6, 16, 7, kBlock, true, SF_DEFER>((m + 15u) / 16u, 0u, stream, arena, arena_bytes, desc + i, m,
+            launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, 0u, stream, arena, arena_bytes, desc + i, m,
                                                           0u, status ? status + i : nullptr, nullptr, ws, fs);
             hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
                                desc + i, m, nh + i, table, (const nfcs_patch*)ws);
@@ -1292,7 +1351,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
     }
     // 7 waves per SIMD (72 VGPRs and 94 SGPRs, no scratch; the compiler alone picks 81 VGPRs
     // and 106 SGPRs = 6 waves and the kernel runs 4-5% slower)
-    launch_rows<6, 16, 7, kBlock, true, SF_INLINE>((n + 15u) / 16u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+    launch_rows<6, 16, 7, kBlock, true, SF_INLINE, 2, 7>((n + 15u) / 16u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
                                                    nullptr, nullptr, fa);
     return hipGetLastError();
 }

@@ -22,9 +22,12 @@ def hinted(engine):
     engine.set_slot_bytes(0)  # the session engine goes back to arena_bytes / n
 
 
-def test_update_every_shape_matches_oracle(hinted):
+@pytest.mark.parametrize("align", [128, 16, 64])
+def test_update_every_shape_matches_oracle(hinted, align):
+    """Also frames that start mid-line (packed 16-byte and 64-byte starts): the long shape reads
+    line-aligned windows (row_stage), whose header view and sums must give the same bytes."""
     frames = oracle.fuzz_frames(33, 0, 70003)  # above kInlineMaxPackets (deferral applies); a partial last wave
-    arena, desc = oracle.pack_frames(frames, align=128)
+    arena, desc = oracle.pack_frames(frames, align=align)
     n = len(desc)
     ref = arena.copy()
     rst, _ = oracle.update_batch(ref, desc, nthreads=8)
@@ -42,9 +45,10 @@ def test_update_every_shape_matches_oracle(hinted):
         b.free()
 
 
-def test_l3_forward_every_shape_matches_oracle(hinted):
+@pytest.mark.parametrize("align", [16, 128])
+def test_l3_forward_every_shape_matches_oracle(hinted, align):
     frames, table, nh = random_l3_case(24, 30001, table_n=8)
-    arena, desc = oracle.pack_frames(frames)
+    arena, desc = oracle.pack_frames(frames, align=align)
     n = len(desc)
     ref = arena.copy()
     rst = oracle.l3_forward_batch(ref, desc, nh, table)
