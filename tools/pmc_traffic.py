@@ -30,13 +30,13 @@ KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("upd
           "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_kernel",)}
 
 
-def run_pass(out, cfg, counters, steps, op="update", packets=0):
+def run_pass(out, cfg, counters, steps, op="update", packets=0, align=128):
     """One rocprofv3 pass with the given counters; per counter, the sum over the op's kernels of
     the median over that kernel's launches."""
-    d = os.path.join(out, f"c{cfg}{'_' + str(packets) if packets else ''}_{op}_{counters[0]}")
-    cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
+    d = os.path.join(out, f"c{cfg}{'_' + str(packets) if packets else ''}_a{align}_{op}_{counters[0]}")
+    cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--op", op] + (["--packets", str(packets)] if packets else [])
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--no-c4", "--op", op, "--align", str(align)] + (["--packets", str(packets)] if packets else [])
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--merge", help="existing traffic.json to extend")
     ap.add_argument("--packets", type=int, default=0,
                     help="packets per launch instead of the config's (C1 with 4194304 = the C4 shard)")
+    ap.add_argument("--align", type=int, default=128, help="frame start alignment (bench.py --align)")
     a = ap.parse_args()
     a.out = os.path.abspath(a.out)  # rocprofv3 runs with cwd /tmp
     os.makedirs(a.out, exist_ok=True)
@@ -76,13 +77,13 @@ def main():
         res = json.load(open(a.merge))
     for cfg, op in [(c, o) for o in a.ops for c in a.configs]:
         P = a.packets
-        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op, P)
-        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op, P)
+        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op, P, a.align)
+        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op, P, a.align)
         q, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
-                        a.steps, op, P)
-        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P)
+                        a.steps, op, P, a.align)
+        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P, a.align)
         key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
-            ("" if op == "update" else f"_{op}")
+            ("" if op == "update" else f"_{op}") + ("" if a.align == 128 else f"_align{a.align}")
         # launches per call: nfcs_update_device runs a long-frame batch of more than 1M packets
         # as 512K-packet sub-batches (kSubBatchPackets), each its own read pass + write pass
         # (the fused forward too, for long frames: read pass + apply_fwd_kernel per sub-batch)
