@@ -1016,7 +1016,7 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
 // LAM: 0 frame-relative windows of K slots; 1 line-aligned windows of KL slots; 2 per wave, line-
 // aligned (KL slots) when a row of the wave starts mid-line, else frame-relative (K slots), so
 // line-aligned batches run the frame-relative code unchanged.
-template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM, int KL>
+template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM = 0, int KL = K>
 __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
                                                               uint32_t nblocks, uint8_t* __restrict__ arena,
                                                               uint64_t arena_bytes, uint32_t base16,
