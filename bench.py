@@ -561,10 +561,11 @@ def main():
     elif fk:
         ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
                                           args.steps) / args.steps
-        # parity: digest of the 64-byte records (they hold the hashes too) vs the reference's
+        # parity: digest of the 64-byte records (they hold the hashes too) vs the reference's; the
+        # records depend on the frames' bytes only, so the digest holds at any --align
         gk = golden().get("flowkey_c1", {})
         want = None
-        if first == 0 and n == gk.get("n") and args.align == gk.get("align"):
+        if args.config == 1 and first == 0 and n == gk.get("n"):
             eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
             rdesc = np.zeros(n, dtype=nf.DESC_DTYPE)
             rdesc["off16"] = np.arange(n, dtype=np.uint32) * 4

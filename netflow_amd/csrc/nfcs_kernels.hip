@@ -1708,7 +1708,11 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
     const uint64_t off = (uint64_t)dl.x * 16u;
     const bool live = p < n && off + (((uint64_t)dl.y + 15u) & ~15ull) <= arena_bytes;
     const uint32_t len = live ? dl.y : 0u;
-    // header lines in 8-lane rows: instruction k, row r -> packet 8k + r, lane rl -> chunk rl (0..5)
+    // Header bytes 0..47 (every field of an IPv4 header without options, tagged or not, and its
+    // ports) in 8-lane rows: instruction k, row r -> packet 8k + r, lane rl -> chunk rl (0..2). A
+    // frame starting up to 80 bytes into a 128-byte line reads that one line (64-byte starts: one
+    // line instead of two; round 3). Headers reaching past byte 47 (IPv6, IPv4 options) load chunks
+    // 3..5 afterwards, lane by lane.
     const uint32_t rl = lane & 7u, r = lane >> 3;
     uint4 c[8];
 #pragma unroll
@@ -1717,15 +1721,31 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
         const uint32_t qo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)dl.x);
         const uint32_t ql = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)len);
         const uint4* src = (const uint4*)(arena + (uint64_t)qo * 16u);
-        c[k] = ld16<0>((rl < 6u && rl * 16u < ql) ? src + rl : &g_zero16);
+        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : &g_zero16);
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k)
-        if (rl < 6u) *(uint4*)(rows + (8u * k + r) * kFkRow + 16u * rl) = c[k];
+        if (rl < 3u) *(uint4*)(rows + (8u * k + r) * kFkRow + 16u * rl) = c[k];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
     __builtin_amdgcn_wave_barrier();
     // lane l parses packet l (extract_flow_key + hash_flow, packet_classifier.cpp:12-108)
-    const uint8_t* b = rows + lane * kFkRow;
+    uint8_t* b = rows + lane * kFkRow;
+    {  // the bytes the key reads end at the ports (IPv4: l2 + IHL*4 + 4; IPv6: l2 + 44)
+        const uint32_t f12 = lds_be16(b, 12), ft = f12 == 0x8100u ? 4u : 0u;
+        const uint32_t fet = (f12 == 0x8100u && len >= 18) ? lds_be16(b, 16) : f12;
+        const uint32_t need = (fet == 0x0800u && 34u + ft <= len) ? 18u + ft + (lds_u8(b, 14u + ft) & 15u) * 4u
+                            : (fet == 0x86DDu && 54u + ft <= len) ? 58u + ft : 0u;
+        const bool more = len >= 14 && need > 48u && len > 48u;
+        if (__builtin_amdgcn_ballot_w64(more) != 0) {
+            if (more) {
+                const uint4* src = (const uint4*)(arena + off);
+#pragma unroll
+                for (uint32_t j = 3; j < 6; ++j) *(uint4*)(b + 16u * j) = ld16<0>(16u * j < len ? src + j : &g_zero16);
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
     const bool eth = len >= 14;
     const uint32_t m0 = eth ? *(const uint32_t*)b : 0u, m1 = eth ? *(const uint32_t*)(b + 4) : 0u;
     const uint32_t m2 = eth ? *(const uint32_t*)(b + 8) : 0u;
