@@ -1398,12 +1398,15 @@ DEV uint32_t dpp_next(uint32_t x) {  // lane rl gets lane rl+1 of its row (0 for
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xF, 0xF, true);
 }
 
-// Edited chunks of one batch. v: old chunks rl + 16k (+ cb); prevw: for a push, the old dword
-// just before this batch (the row's lane 15 of the previous batch); nextx: for a pop, the old
-// dword just after it. Batch 0 (first = true) builds the new bytes 12-15 in chunk 0.
+// Edited chunks of one batch. v: old chunks rl + 16k (+ cb) of the row's window, i.e. frame chunks
+// rl + 16k + cb - mis (line-aligned windows: the frame's chunk 0 sits in lane mis of slot 0);
+// prevw: for a push, the old dword just before this batch (the row's lane 15 of the previous
+// batch); nextx: for a pop, the old dword just after it. Batch 0 (first = true) builds the new
+// bytes 12-15 in chunk 0. Lanes before the frame start get values that are never stored or summed.
 template <int K, int R = 16>
 DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t rl, bool first,
-                   uint32_t prevw, uint32_t nextx, uint32_t tag_dw, uint32_t cb, uint32_t wend) {
+                   uint32_t prevw, uint32_t nextx, uint32_t tag_dw, uint32_t cb, uint32_t wend,
+                   uint32_t mis = 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint4 e = v[k];
@@ -1412,18 +1415,18 @@ DEV void vlan_edit(uint4 (&nv)[K], const uint4 (&v)[K], uint32_t mode, uint32_t 
             const uint32_t lw = (k > 0) ? row_bcast<R - 1, R>(v[k - 1].w) : prevw;
             if (rl == 0) pw = lw;
             e = make_uint4(pw, v[k].x, v[k].y, v[k].z);
-            if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, tag_dw);
+            if (first && k == 0 && rl == mis) e = make_uint4(v[0].x, v[0].y, v[0].z, tag_dw);
         } else if (mode == VM_POP) {  // new[o] = old[o + 4] for o >= 12
             uint32_t nx = dpp_next(v[k].x);  // across an 8-lane row's end: replaced below
             const uint32_t fx = (k + 1 < K) ? row_bcast<0, R>(v[k + 1 < K ? k + 1 : k].x) : nextx;
             if (rl == (uint32_t)R - 1u) nx = fx;
             e = make_uint4(v[k].y, v[k].z, v[k].w, nx);
-            if (first && k == 0 && rl == 0) e = make_uint4(v[0].x, v[0].y, v[0].z, nx);
+            if (first && k == 0 && rl == mis) e = make_uint4(v[0].x, v[0].y, v[0].z, nx);
         } else if (mode == VM_RETAG) {
-            if (first && k == 0 && rl == 0) e.w = tag_dw;
+            if (first && k == 0 && rl == mis) e.w = tag_dw;
         }
-        const uint32_t c = cb + rl + (uint32_t)R * (uint32_t)k;
-        nv[k] = keep_tail(e, v[k], 16u * c, wend);
+        const uint32_t c = cb + rl + (uint32_t)R * (uint32_t)k - mis;
+        nv[k] = (int)c < 0 ? v[k] : keep_tail(e, v[k], 16u * c, wend);
     }
 }
 
@@ -1441,7 +1444,28 @@ DEV void vst8(uint8_t* p, uint32_t b) {
     else st8<POL == VST_WT>(p, b);
 }
 
-template <int K, int K2 = 2, int POL = VST_PLAIN, int R = 16>
+// Frame chunk rl (rl < R) of a row whose window is line-aligned (slot 0 lane rl + mis, or slot 1).
+template <int K, int R>
+DEV uint4 vlan_view(const uint4 (&v)[K], uint32_t rowbase4, uint32_t rl, uint32_t mis) {
+    const uint32_t a = rl + mis;
+    const int sl = (int)(rowbase4 + (a & (R - 1)) * 4u);
+    const uint4 r0 = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[0].x),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[0].y),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[0].z),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[0].w));
+    const uint4 r1 = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[1].x),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[1].y),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[1].z),
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[1].w));
+    return a < (uint32_t)R ? r0 : r1;
+}
+
+// LA: line-aligned windows as in the checksum kernel (row_stage): lane rl of slot k holds frame
+// chunk 16k + rl - mis, so every load and store instruction covers whole lines whatever the frame's
+// line offset; the 4-byte moves are the same lane shifts in these coordinates, and the header views
+// the edit and the plan read are rotated into frame order (vlan_view) in waves with a row starting
+// mid-line.
+template <int K, int K2 = 2, int POL = VST_PLAIN, int R = 16, bool LA = false>
 __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__ arena,
                                                            uint64_t arena_bytes,
                                                            nfcs_desc* __restrict__ desc, uint32_t n,
@@ -1483,18 +1507,24 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     uint8_t* frame = arena + (live ? off : 0);
     const uint4* src = (const uint4*)frame;
     const uint32_t nl = live ? (uint32_t)((need + 15u) >> 4) : 0u;  // old chunks to load
+    // a row takes line-aligned windows only where they need no more row passes than frame-relative
+    // ones (a 1500-byte frame 48+ bytes into a line would spill into a second pass: 64-byte starts
+    // measured 0.47 against 0.71 with it)
+    const uint32_t lm = LA && live ? (uint32_t)(((uintptr_t)frame >> 4) & 7u) : 0u;
+    const uint32_t mis = (nl + lm <= KR || nl > KR) ? lm : 0u;
+    const bool rot = LA && __builtin_amdgcn_ballot_w64(mis != 0) != 0;  // wave-uniform
 
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t c = rl + (uint32_t)R * k;
+        const uint32_t c = rl + (uint32_t)R * k - mis;  // frame chunk (wraps below the frame start)
         v[k] = ld16<0>((c < nl) ? src + c : &g_zero16);
     }
-    // pop: the old dword after batch 0 (first dword of chunk KR)
-    const uint32_t nx0 = *(const uint32_t*)((KR < nl) ? src + KR : &g_zero16);
+    // pop: the old dword after batch 0 (first dword of the window's chunk KR)
+    const uint32_t nx0 = *(const uint32_t*)((KR - mis < nl) ? src + (KR - mis) : &g_zero16);
 
     // the edit the reference makes (packet.hpp:655-720), decided on the old header
-    const RowHdr<R> h{v[0], rowbase4};
+    const RowHdr<R> h{rot ? vlan_view<K, R>(v, rowbase4, rl, mis) : v[0], rowbase4};
     const bool tagged = len >= 14 && h.be16(12) == 0x8100u;  // has_vlan() (603-606)
     uint32_t mode = VM_NONE;
     if (live && kind == NFCS_VLAN_PUSH)
@@ -1513,11 +1543,11 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     const uint32_t nst = !act ? 0u : mode == VM_RETAG ? 1u : (wend + 15u) >> 4;  // chunks stored
 
     uint4 nv[K];
-    vlan_edit<K, R>(nv, v, mode, rl, true, 0u, nx0, tag_dw, 0u, wend);
+    vlan_edit<K, R>(nv, v, mode, rl, true, 0u, nx0, tag_dw, 0u, wend, mis);
     uint32_t carry = row_bcast<R - 1, R>(v[K - 1].w);  // push: old dword before batch 1
 
     // update_checksums() on the edited frame (690 / 718)
-    RPlan P = fast_plan<R>(nv[0], rowbase4, nlen);
+    RPlan P = fast_plan<R>(rot ? vlan_view<K, R>(nv, rowbase4, rl, mis) : nv[0], rowbase4, nlen);
     const bool slow = act && (P.st >> 8) != 0;
     if (!act || slow) P = rplan_none(0);
     const uint32_t re = (P.flags & F_L4) ? P.re : 0u, lo4 = P.rs & ~3u;
@@ -1526,11 +1556,14 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     asm volatile("" : "+v"(rlv));
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc_slot(acc, nv[k], rlv + (uint32_t)R * k, lo4, re, tailfix);
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = rlv + (uint32_t)R * k - mis;
+        if ((int)c >= 0) acc_slot(acc, nv[k], c, lo4, re, tailfix);
+    }
 
     // rows whose frame continues past batch 0 (moved chunks or summed chunks)
     const uint32_t nre = (re + 15u) >> 4;
-    const uint32_t cm = (nst > nre) ? nst : nre;
+    const uint32_t cm = ((nst > nre) ? nst : nre) + mis;  // window chunks
     const bool multi = __builtin_amdgcn_ballot_w64(cm > KR) != 0;  // wave-uniform
     auto finish = [&](uint32_t a) -> uint32_t {  // l4 field word
         const uint32_t z = row_sum<R>(a) + P.corr;
@@ -1545,25 +1578,33 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
         // checksum bytes into the chunk registers (fast-path fields lie below byte 80: slot 0);
         // a re-tag stores chunk 0 and the chunks holding checksum bytes
         // (byte by byte: put_field measured 1.2% slower here, 0.723 against 0.732 on C1)
-        bool patched = false;
+        // (with line-aligned windows the chunk of byte pos sits in lane (pos/16 + mis) % R of slot
+        // (pos/16 + mis) / R: slot 0, or slot 1 of an 8-lane row)
+        bool patched0 = false, patched1 = false;
 #pragma unroll
         for (uint32_t t = 0; t < 4; ++t) {
             const uint32_t w = (t < 2) ? ipw : l4w;
             const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl) {
-                nv[0] = put_byte(nv[0], pos & 15u, (w >> (16 + 8 * (t & 1u))) & 0xFFu);
-                patched = true;
+            const uint32_t a = (pos >> 4) + mis, b = (w >> (16 + 8 * (t & 1u))) & 0xFFu;
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (a & (R - 1)) == rl) {
+                if (a < (uint32_t)R) {
+                    nv[0] = put_byte(nv[0], pos & 15u, b);
+                    patched0 = true;
+                } else {
+                    nv[1] = put_byte(nv[1], pos & 15u, b);
+                    patched1 = true;
+                }
             }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t c = rl + (uint32_t)R * k;
-            if (c < nst || (k == 0 && patched)) vst16<POL>((uint4*)frame + c, nv[k]);
+            const uint32_t c = rl + (uint32_t)R * k - mis;
+            if (c < nst || (k == 0 && patched0) || (k == 1 && patched1)) vst16<POL>((uint4*)frame + c, nv[k]);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t c = rl + (uint32_t)R * k;
+            const uint32_t c = rl + (uint32_t)R * k - mis;
             if (c < nst) vst16<POL>((uint4*)frame + c, nv[k]);
         }
         const uint32_t cmax = wave_max_rows<R>(cm);
@@ -1574,15 +1615,15 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
             uint4 w[K2], e[K2];
 #pragma unroll
             for (int k = 0; k < K2; ++k) {
-                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                const uint32_t c = cb + rlv + (uint32_t)R * k - mis;
                 w[k] = ld16<1>((c < nl) ? src + c : &g_zero16);
             }
-            const uint32_t nx = *(const uint32_t*)((cb + KR2 < nl) ? src + cb + KR2 : &g_zero16);
-            vlan_edit<K2, R>(e, w, mode, rl, false, carry, nx, 0u, cb, wend);
+            const uint32_t nx = *(const uint32_t*)((cb + KR2 - mis < nl) ? src + (cb + KR2 - mis) : &g_zero16);
+            vlan_edit<K2, R>(e, w, mode, rl, false, carry, nx, 0u, cb, wend, mis);
             carry = row_bcast<R - 1, R>(w[K2 - 1].w);
 #pragma unroll
             for (int k = 0; k < K2; ++k) {
-                const uint32_t c = cb + rlv + (uint32_t)R * k;
+                const uint32_t c = cb + rlv + (uint32_t)R * k - mis;
                 acc_slot(acc, e[k], c, lo4, re, tailfix);
                 if (c < nst) vst16<POL>((uint4*)frame + c, e[k]);
             }
@@ -1593,7 +1634,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
         for (uint32_t t = 0; t < 4; ++t) {
             const uint32_t w = (t < 2) ? ipw : l4w;
             const uint32_t pos = (w & 0xFFFFu) + (t & 1u);
-            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (pos >> 4) == rl)
+            if ((w & 0xFFFFu) != NFCS_PATCH_NONE && (((pos >> 4) + mis) & (R - 1)) == rl)
                 vst8<POL>(frame + pos, w >> (16 + 8 * (t & 1u)));
         }
     }
@@ -1665,7 +1706,7 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
                            desc, n, ops, op_all, caps, cap_all, status, obs);
     else  // 4 rows per wave, 4 waves per workgroup
-        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT>), g16, dim3(kBlock), 0, stream, arena, arena_bytes,
+        hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 16, true>), g16, dim3(kBlock), 0, stream, arena, arena_bytes,
                            desc, n, ops, op_all, caps, cap_all, status, obs);
     return hipGetLastError();
 }

@@ -6,7 +6,8 @@ that mapping changes — the end of slot 0 (256 bytes), the 7 slots of one row p
 continuation batches of jumbo frames — and with every header kind of the fuzz generator (802.1Q,
 IPv6, ICMP, IP options and IHL < 5 for the cold path, runts), in waves that mix aligned and
 misaligned rows. The update (long shape forced by the slot-size hint, above kInlineMaxPackets so
-deferred waves take part), the fused L3 forward and the flow keys must equal the oracle."""
+deferred waves take part), the fused L3 forward, VLAN push / pop and the flow keys must equal the
+oracle."""
 import numpy as np
 import pytest
 
@@ -130,4 +131,36 @@ def test_flow_keys_every_line_offset(engine):
     assert np.array_equal(d_hash.download(np.uint32, n), hashes)
     assert np.array_equal(d_keys.download(np.uint8, 64 * n).reshape(n, 64), np.asarray(keys).reshape(n, 64))
     for b in (d_arena, d_desc, d_keys, d_hash):
+        b.free()
+
+
+def test_vlan_every_line_offset(long_shape):
+    """VLAN push / pop / re-tag with line-aligned windows (vlan_rows_kernel, long shape): frames at
+    every line offset, lengths around the slot boundaries and the fuzz generator's header kinds,
+    each with room for a push; bytes, lengths and statuses equal the oracle's."""
+    import netflow_amd as nf
+    from vlan_common import random_vlan_case
+    rng = np.random.default_rng(29)
+    bf = boundary_frames(rng)
+    fr, ops, caps = random_vlan_case(31, 30000)
+    frames = bf * 8 + fr
+    kinds = [oracle.vlan_op("push", 100, 3), oracle.vlan_op("pop"), oracle.vlan_op("push", 7, 1)]
+    ops = np.concatenate([np.array([kinds[i % 3] for i in range(8 * len(bf))], dtype=np.uint32), ops])
+    caps = np.concatenate([np.array([len(f) + 4 for f in bf * 8], dtype=np.uint32), caps])
+    offsets = np.concatenate([np.repeat(np.arange(8), len(bf)), rng.integers(0, 8, len(fr))])
+    arena, desc = place(frames, offsets, room=4)
+    n = len(desc)
+    ref, rdesc = arena.copy(), desc.copy()
+    rst = oracle.vlan_batch(ref, rdesc, ops=ops, caps=caps)
+    d_arena = long_shape.alloc(arena.nbytes).upload(arena)
+    d_desc = long_shape.alloc(desc.nbytes).upload(desc)
+    d_ops = long_shape.alloc(ops.nbytes).upload(ops)
+    d_caps = long_shape.alloc(caps.nbytes).upload(caps)
+    d_st = long_shape.alloc(n)
+    long_shape.vlan_device(d_arena, arena.nbytes, d_desc, n, d_ops, 0, d_caps, 0, d_st)
+    long_shape.sync()
+    assert np.array_equal(d_st.download(np.uint8, n), rst)
+    assert np.array_equal(d_desc.download(nf.DESC_DTYPE, n), rdesc)
+    assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref)
+    for b in (d_arena, d_desc, d_ops, d_caps, d_st):
         b.free()
