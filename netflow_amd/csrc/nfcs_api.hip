@@ -58,12 +58,15 @@ struct nfcs_ctx {
     uint64_t* d_digest = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // patch records of the waves that defer their stores (kUpdateAuto without a caller d_patch),
-    // grown on demand; ws_ev marks the last launch that used it, on ws_stream
+    // grown on demand; its last user ran on ws_stream (ws_own: the context's own stream). ws_ev
+    // marks that user's write pass: recorded by the call itself on a caller's stream, and only when
+    // another stream comes along on the context's own one (acquire_ws)
     nfcs_patch* ws = nullptr;
     size_t ws_cap = 0;  // records
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
+    bool ws_own = false;
     uint32_t slot_bytes = 0;  // launch-shape hint (nfcs_ctx_set_slot_bytes); 0 = arena_bytes / n
     // the footprint observation (launch_shape): host-mapped u32 the kernels write, and the
     // descriptor array it belongs to
@@ -79,10 +82,22 @@ thread_local int g_last_hip = 0;
 // The deferred-store workspace for a launch of n packets on `st`. A launch on another stream
 // than the previous user first waits (on the device) for that user's write pass, so calls on one
 // context from several streams never overwrite each other's records; growing it waits on the host.
+// A previous user on the context's own stream gets its event here, when it is needed: that stream
+// lives as long as the context, and an event recorded now follows all its work. So back-to-back
+// calls on one stream queue nothing between their kernels (an event per call cost C1 ~6 µs of idle
+// GPU between calls, 1.5-2%; round 3, profiles/r03_s3_ab_ws_event.jsonl).
+hipError_t wait_ws_user(nfcs_ctx* c, hipStream_t st) {
+    if (c->ws_own) {
+        hipError_t e = hipEventRecord(c->ws_ev, c->stream);
+        if (e != hipSuccess) return e;
+    }
+    return st ? hipStreamWaitEvent(st, c->ws_ev, 0) : hipEventSynchronize(c->ws_ev);
+}
+
 hipError_t acquire_ws(nfcs_ctx* c, size_t n, hipStream_t st) {
     if (n > c->ws_cap) {
         if (c->ws_used) {
-            hipError_t e = hipEventSynchronize(c->ws_ev);
+            hipError_t e = wait_ws_user(c, nullptr);  // on the host: the buffer is freed next
             if (e != hipSuccess) return e;
         }
         if (c->ws) (void)hipFree(c->ws);
@@ -94,7 +109,7 @@ hipError_t acquire_ws(nfcs_ctx* c, size_t n, hipStream_t st) {
         if (e != hipSuccess) return e;
         c->ws_cap = cap;
     } else if (c->ws_used && c->ws_stream != st) {
-        hipError_t e = hipStreamWaitEvent(st, c->ws_ev, 0);
+        hipError_t e = wait_ws_user(c, st);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -102,7 +117,9 @@ hipError_t acquire_ws(nfcs_ctx* c, size_t n, hipStream_t st) {
 hipError_t release_ws(nfcs_ctx* c, hipStream_t st) {
     c->ws_stream = st;
     c->ws_used = true;
-    return hipEventRecord(c->ws_ev, st);
+    c->ws_own = st == c->stream;
+    // a caller's stream may be gone by the time another stream comes: its event is recorded now
+    return c->ws_own ? hipSuccess : hipEventRecord(c->ws_ev, st);
 }
 
 int hip_fail(hipError_t e) {
@@ -485,6 +502,7 @@ NFCS_API int nfcs_ctx_destroy(nfcs_ctx* c) {
     if (!c) return NFCS_OK;
     DeviceGuard dg_(c->di.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ws_used && !c->ws_own && c->ws_ev) (void)hipEventSynchronize(c->ws_ev);  // a caller stream's last write pass
     free_host_pipeline(c);
     if (c->d_digest) (void)hipFree(c->d_digest);
     if (c->ws) (void)hipFree(c->ws);

@@ -117,10 +117,12 @@ def test_c4_shard_digest_large_arena(engine, rank):
 
 
 def test_two_streams_share_the_workspace(engine):
-    """Back-to-back calls on one context from two streams, no caller patch records: both use the
-    context's deferred-store workspace; the second stream waits for the first's write pass. The
-    streams come from the HIP runtime libnfcs.so is bound to: opened by its SONAME, the loader
-    returns the copy already in the process."""
+    """Back-to-back calls on one context from two caller streams and the context's own stream, no
+    caller patch records: all use the context's deferred-store workspace; each call on another
+    stream than the previous one waits for that one's write pass (a caller stream's event is
+    recorded by its call; the own stream's only when another stream comes). The streams come from
+    the HIP runtime libnfcs.so is bound to: opened by its SONAME, the loader returns the copy
+    already in the process."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so.7")
     g = json.load(open(os.path.join(GOLD, "configs.json")))
@@ -139,18 +141,22 @@ def test_two_streams_share_the_workspace(engine):
     s1, s2 = _S(streams[0]), _S(streams[1])
     b1 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
     b2 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
-    for _ in range(3):
-        engine.gen_config_device(1, g["seed"], 0, 1 << 20, b1[0], b1[1], b1[2])
-        engine.gen_config_device(1, g["seed"], 0, 1 << 20, b2[0], b2[1], b2[2])
+    b0 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
+    b3 = engine.config_batch(1, g["seed"], 0, 1 << 20, 128)
+    want = g["configs"]["1"]["digest_out"]
+    for order in ((s1, s2), (None, s1, None, s2), (s1, None, s2, None)):
+        bs = (b1, b2) if len(order) == 2 else (b0, b1, b3, b2)
+        for b in bs:
+            engine.gen_config_device(1, g["seed"], 0, 1 << 20, b[0], b[1], b[2])
         engine.sync()
-        engine.update_device(b1[0], b1[1], b1[2], 1 << 20, stream=s1.cuda_stream)
-        engine.update_device(b2[0], b2[1], b2[2], 1 << 20, stream=s2.cuda_stream)
+        for b, st in zip(bs, order):  # no host sync between the calls
+            engine.update_device(b[0], b[1], b[2], 1 << 20, stream=None if st is None else st.cuda_stream)
         s1.synchronize()
         s2.synchronize()
-        want = g["configs"]["1"]["digest_out"]
-        for b in (b1, b2):
+        engine.sync()
+        for b in bs:
             assert f"{engine.digest_device(b[0], b[1], b[2], 1 << 20, 0):016x}" == want
-    for b in (b1, b2):
+    for b in (b0, b1, b2, b3):
         b[0].free()
         b[2].free()
     for st in streams:
