@@ -29,8 +29,9 @@ enum : int {
     kUpdateInline = 2    // every wave stores inline (the zero-copy host path: frames over PCIe)
 };
 
-// A wave whose four frames average at least this many bytes defers its checksum stores to the
-// write pass (kUpdateAuto). Uniform-length sweeps (tools/exp/len_sweep.sh, 1M frames, DESIGN.md
+// In the long shape (mean footprint >= kSmallMeanBytes) a wave whose four frames average at least
+// this many bytes defers its checksum stores to the write pass (kUpdateAuto); the short and tiny
+// shapes store every wave inline (round 3: no write pass for them, launch_update_one). Uniform-length sweeps (tools/exp/len_sweep.sh, 1M frames, DESIGN.md
 // §5e): at 1024 B inline stores win (0.661 vs 0.635), at 1280 B deferral wins (replayed 0.782 vs
 // 0.768, fresh 0.760 vs 0.624), at 1500 B too (0.759 / 0.745 vs 0.757 / 0.653). Short frames' reads
 // are latency-bound and hide the inline stores; a mixed batch like C3 (U{64..1500}) lost 3.5% when

@@ -1092,7 +1092,6 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* _
 // (its record and frame offset by ds_bpermute), so the packet's 4 bytes leave in one store
 // instruction as one write request with a byte mask. An IPv4 byte that the L4 field overlaps
 // (IHL < 5) is left to the L4 lane: the reference writes the L4 field last.
-template <bool EARLY>
 __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict__ arena,
                                                              const nfcs_desc* __restrict__ desc,
                                                              uint32_t n, uint32_t base16,
@@ -1100,20 +1099,17 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
-    // EARLY (batches of long frames, where most waves defer): the record is loaded with the
-    // descriptor, before the decision — one memory round trip ahead of the stores instead of two
-    // (C1 +1.5%, the 4M shard +0.5%; records of waves that stored inline are stale and ignored).
-    // Short-frame batches, where almost no wave defers, load only the deferred packets' records
-    // (C3: 10 µs instead of 14 µs for this pass).
+    // The record is loaded with the descriptor, before the decision — one memory round trip ahead
+    // of the stores instead of two (C1 +1.5%, the 4M shard +0.5%; records of waves that stored
+    // inline are stale and ignored). Only the long shape runs this pass (launch_update_one).
     uint2 r0 = make_uint2(0u, 0u);
-    if (EARLY && i < n) r0 = ((const uint2*)rec)[i];
+    if (i < n) r0 = ((const uint2*)rec)[i];
     uint32_t s = defer_len(d.len);
     s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
     s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
     const bool dfr = i < n && defer_group(s, 4);
     const uint64_t mask = __builtin_amdgcn_ballot_w64(dfr);
     if (!mask) return;
-    if (!EARLY && dfr) r0 = ((const uint2*)rec)[i];
     const uint2 r = dfr ? r0 : make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
     const uint32_t j = lane & 3u;
 #pragma unroll
@@ -1256,14 +1252,17 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
         NFCS_ROWS(1, kBlock, g4, SF_RECORDS);
     } else if (form == kUpdateInline) {
         NFCS_SHAPED(SF_INLINE);
+    } else if (shape != kShapeLong) {
+        // short and tiny shapes: every wave stores inline and no write pass is launched. The few
+        // groups of 4 that average >= kDeferMeanBytes in such batches gain less from deferral than
+        // the write pass costs to find them among all the descriptors (round 3, same box: C3 +1.5-2.4%,
+        // 1M x 64 B +5.5%, 4M mixes of 64/1500-byte frames with 25/50/75% long frames +2/+1.3/+3.7%;
+        // profiles/r03_s3_ab_c3_inline.jsonl, r03_s3_ab_bimodal.jsonl)
+        NFCS_SHAPED(SF_INLINE);
     } else {
-        NFCS_SHAPED(SF_DEFER);
-        if (shape != kShapeLong)
-            hipLaunchKernelGGL(apply_bytes_kernel<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                               stream, arena, desc, n, base16, patch ? patch : ws);
-        else
-            hipLaunchKernelGGL(apply_bytes_kernel<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                               stream, arena, desc, n, base16, patch ? patch : ws);
+        NFCS_ROWS(1, kBlock, g4, SF_DEFER);
+        hipLaunchKernelGGL(apply_bytes_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                           arena, desc, n, base16, patch ? patch : ws);
     }
 #undef NFCS_SHAPED
 #undef NFCS_ROWS8
