@@ -47,86 +47,66 @@
 
 namespace netflow_amd {
 
-// Same layout and semantics as netflow::PacketBuffer (packet_buffer.hpp:10-111).
-struct PacketBuffer {
-    unsigned char* raw_data_ptr_;
-    size_t capacity_;
-    size_t data_offset_;
-    size_t data_len_;
-    std::atomic<int> ref_count;
+// The caller-facing contract of netflow::PacketBuffer (packet_buffer.hpp:10-111): the same
+// constructor arguments, accessors, ref_count and refcount calls, bool results of the window edits,
+// and exception types (std::invalid_argument from the constructor, std::out_of_range from
+// reset_offsets_and_len). Held here as a window [head_, head_ + len_) into cap_ bytes of storage
+// that the buffer owns, or, built External, borrows (a BufferPool's pinned arena slot).
+class PacketBuffer {
+public:
+    std::atomic<int> ref_count{1};
 
     PacketBuffer(size_t capacity, size_t initial_headroom = 0, size_t initial_data_len = 0)
-        : raw_data_ptr_(new unsigned char[capacity]),
-          capacity_(capacity),
-          data_offset_(initial_headroom),
-          data_len_(initial_data_len),
-          ref_count(1) {
-        if (initial_headroom + initial_data_len > capacity) {
-            delete[] raw_data_ptr_;
-            throw std::invalid_argument("Initial headroom + data length exceeds capacity");
-        }
-    }
-    // Non-owning form: the bytes belong to someone else (a BufferPool's pinned arena slot).
+        : owned_(window_fits(capacity, initial_headroom, initial_data_len, "PacketBuffer")
+                     ? new unsigned char[capacity] : nullptr),
+          base_(owned_.get()), cap_(capacity), head_(initial_headroom), len_(initial_data_len) {}
     struct External {};
     PacketBuffer(External, unsigned char* storage, size_t capacity, size_t initial_headroom = 0,
                  size_t initial_data_len = 0)
-        : raw_data_ptr_(storage),
-          capacity_(capacity),
-          data_offset_(initial_headroom),
-          data_len_(initial_data_len),
-          ref_count(1),
-          owns_(false) {
-        if (initial_headroom + initial_data_len > capacity)
-            throw std::invalid_argument("Initial headroom + data length exceeds capacity");
-    }
-    ~PacketBuffer() {
-        if (owns_) delete[] raw_data_ptr_;
-    }
+        : base_(window_fits(capacity, initial_headroom, initial_data_len, "PacketBuffer(External)")
+                    ? storage : nullptr),
+          cap_(capacity), head_(initial_headroom), len_(initial_data_len) {}
     PacketBuffer(const PacketBuffer&) = delete;
     PacketBuffer& operator=(const PacketBuffer&) = delete;
 
     void increment_ref() { ref_count.fetch_add(1, std::memory_order_relaxed); }
+    // true when this call dropped the last reference
     bool decrement_ref() { return ref_count.fetch_sub(1, std::memory_order_acq_rel) == 1; }
 
-    unsigned char* get_data_start_ptr() const { return raw_data_ptr_ + data_offset_; }
-    size_t get_data_length() const { return data_len_; }
-    size_t get_capacity() const { return capacity_; }
-    size_t get_headroom() const { return data_offset_; }
-    size_t get_tailroom() const { return capacity_ - (data_offset_ + data_len_); }
+    unsigned char* get_data_start_ptr() const { return base_ + head_; }
+    size_t get_data_length() const { return len_; }
+    size_t get_capacity() const { return cap_; }
+    size_t get_headroom() const { return head_; }
+    size_t get_tailroom() const { return cap_ - head_ - len_; }
+    unsigned char* storage() const { return base_; }  // byte 0 of the capacity
 
-    bool set_data_len(size_t new_len) {
-        if (data_offset_ + new_len <= capacity_) {
-            data_len_ = new_len;
-            return true;
-        }
-        return false;
-    }
-    bool prepend_data(size_t n) {
-        if (get_headroom() >= n) { data_offset_ -= n; data_len_ += n; return true; }
-        return false;
-    }
-    bool append_data(size_t n) {
-        if (get_tailroom() >= n) { data_len_ += n; return true; }
-        return false;
-    }
-    bool consume_data_front(size_t n) {
-        if (data_len_ >= n) { data_offset_ += n; data_len_ -= n; return true; }
-        return false;
-    }
-    bool consume_data_end(size_t n) {
-        if (data_len_ >= n) { data_len_ -= n; return true; }
-        return false;
-    }
+    // Window edits: false (and no change) when the new window would leave [0, capacity).
+    bool set_data_len(size_t n) { return place(head_, n); }
+    bool append_data(size_t n) { return n <= get_tailroom() && place(head_, len_ + n); }
+    bool prepend_data(size_t n) { return n <= head_ && place(head_ - n, len_ + n); }
+    bool consume_data_front(size_t n) { return n <= len_ && place(head_ + n, len_ - n); }
+    bool consume_data_end(size_t n) { return n <= len_ && place(head_, len_ - n); }
     void reset_offsets_and_len(size_t new_offset, size_t new_len) {
-        if (new_offset + new_len <= capacity_) {
-            data_offset_ = new_offset;
-            data_len_ = new_len;
-        } else {
-            throw std::out_of_range("New offset and length exceed buffer capacity in reset_offsets_and_len");
-        }
+        if (!place(new_offset, new_len))
+            throw std::out_of_range("netflow_amd::PacketBuffer::reset_offsets_and_len: window past capacity");
     }
 
-    bool owns_ = true;  // false: storage not allocated by this buffer
+private:
+    static bool window_fits(size_t cap, size_t head, size_t len, const char* who) {
+        if (len > cap || head > cap - len)
+            throw std::invalid_argument(std::string("netflow_amd::") + who + ": headroom + data length > capacity");
+        return true;
+    }
+    bool place(size_t head, size_t len) {
+        if (len > cap_ || head > cap_ - len) return false;
+        head_ = head;
+        len_ = len;
+        return true;
+    }
+
+    std::unique_ptr<unsigned char[]> owned_;
+    unsigned char* base_;
+    size_t cap_, head_, len_;
 };
 
 class Packet;
@@ -610,7 +590,7 @@ public:
     }
 
     bool in_arena(const PacketBuffer* b) const {
-        return b && b->raw_data_ptr_ >= arena_ && b->raw_data_ptr_ < arena_ + slots_ * slot_bytes_;
+        return b && b->storage() >= arena_ && b->storage() < arena_ + slots_ * slot_bytes_;
     }
     size_t available() {
         std::lock_guard<std::mutex> lock(mu_);
@@ -627,7 +607,7 @@ public:
 
 private:
     uint32_t slot_of(const PacketBuffer* b) const {
-        return static_cast<uint32_t>((b->raw_data_ptr_ - arena_) / slot_bytes_);
+        return static_cast<uint32_t>((b->storage() - arena_) / slot_bytes_);
     }
 
     ChecksumEngine& eng_;

@@ -42,6 +42,13 @@ static int cpu_checks() {
     bad += !pb.set_data_len(96) || pb.set_data_len(97);
     bad += !pb.prepend_data(4) || pb.get_data_length() != 100 || pb.get_headroom() != 28;
     bad += !pb.consume_data_front(4) || !pb.consume_data_end(4) || pb.get_data_length() != 92;
+    bad += pb.append_data(5) || !pb.append_data(4) || pb.get_tailroom() != 0 || pb.prepend_data(33);
+    bad += pb.consume_data_front(97) || pb.consume_data_end(~size_t(0)) || pb.append_data(~size_t(0));
+    bad += !pb.consume_data_end(4) || pb.get_data_length() != 92 || pb.get_headroom() != 32;
+    try { pb.reset_offsets_and_len(100, 29); bad += 1; } catch (const std::out_of_range&) {}
+    pb.reset_offsets_and_len(100, 28);
+    bad += pb.get_headroom() != 100 || pb.get_tailroom() != 0 || pb.get_data_start_ptr() != pb.storage() + 100;
+    pb.reset_offsets_and_len(32, 92);
     {
         Packet p(&pb);
         bad += pb.ref_count != 2 || p.get_buffer() != &pb;
@@ -85,7 +92,7 @@ static int vlan_mode(bool single) {
         std::vector<uint8_t> f = unhex(line.substr(b + 1));
         // headroom 32 as the reference's BufferPool allocates (buffer_pool.hpp:57)
         bufs.emplace_back(new netflow_amd::PacketBuffer(room.back() + 32, 32, f.size()));
-        std::memset(bufs.back()->raw_data_ptr_, 0, room.back() + 32);
+        std::memset(bufs.back()->storage(), 0, room.back() + 32);
         if (!f.empty()) std::memcpy(bufs.back()->get_data_start_ptr(), f.data(), f.size());
         pkts.emplace_back(new netflow_amd::Packet(bufs.back().get()));
     }
