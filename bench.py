@@ -343,16 +343,23 @@ def cpu_baseline(config: int, threads: int = 0, min_seconds: float = 10.0, op: s
     unit, scale = ("Mpkt/s", n / 1e6) if op == "flowkey" else ("GB/s", nbytes / 1e9)
     reps, el = timed(t_all, min_seconds)
     reps1, el1 = timed(1, one_core_seconds)
-    out = {"value": round(scale * reps / el, 3), "unit": unit, "cores": t_all, "kind": kind,
-           "one_core": round(scale * reps1 / el1, 3), **info}
+    runs = {t_all: (reps, el)}
     quota = info.get("cgroup_cpu_quota")
     q = int(quota) if quota else 0
     note = ""
     if not port and 1 < q < t_all:
-        repsq, elq = timed(q, quota_seconds)
-        out["at_quota_threads"] = {"threads": q, "value": round(scale * repsq / elq, 3)}
+        # the cgroup grants q CPUs of run time: t_all threads share that much, q threads may not
+        runs[q] = timed(q, quota_seconds)
         note = (f"; the cgroup grants {quota:g} CPUs of run time, so {t_all} threads share that much; "
-                f"{q} threads: x {repsq} passes ({elq:.1f} s)")
+                f"{q} threads: x {runs[q][0]} passes ({runs[q][1]:.1f} s)")
+    rates = {t: scale * r / e for t, (r, e) in runs.items()}
+    best = max(rates, key=rates.get)  # the fastest thread count measured is the baseline
+    out = {"value": round(rates[best], 3), "unit": unit, "cores": best, "kind": kind,
+           "one_core": round(scale * reps1 / el1, 3),
+           "runs": [{"threads": t, "value": round(v, 3)} for t, v in sorted(rates.items())],
+           "selection": "value = the fastest of the thread counts measured (every allotted CPU; as "
+                        "many threads as the cgroup's CPU quota when it grants fewer); cores = its threads",
+           **info}
     out["sample"] = (f"{n} packets of config C{config} ({nbytes / 1e6:.0f} MB) x {reps} passes on "
                      f"{t_all} threads pinned over the allotted CPUs ({el:.1f} s) and x {reps1} on 1 thread "
                      f"({el1:.1f} s), g++ -O2" + note)
@@ -408,6 +415,7 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch sub-line")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the C4-shard sub-line")
+    ap.add_argument("--no-host", action="store_true", help="N = 1: skip the host-memory (PCIe) sub-line")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -697,6 +705,8 @@ def main():
         d_arena.free()
         d_arena = None
         out["c4_shard"] = c4_shard_line(eng, args)
+        if not args.no_host:
+            out["host"] = host_line(eng, args, n)
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
@@ -781,9 +791,11 @@ def c4_shard_line(eng, args):
 
 
 def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc):
-    """The same work rotated over FRESH_BATCHES separately generated batches (the timed one plus
-    FRESH_BATCHES - 1 more), so no launch runs over what the previous launch just wrote, as in a
-    NIC ring's steady state; wall clock around the steps, digests of every batch afterwards."""
+    """The steady state of a NIC ring: the same work rotated over FRESH_BATCHES separately generated
+    batches (the timed one plus FRESH_BATCHES - 1 more), so no call runs over what the previous call
+    just wrote and no header line is still in the memory-side cache from a previous pass over the
+    same batch. Wall clock around the steps, then the same rotation timed by HIP events on the
+    engine's stream (nfcs_time_update_batches: `frac`), then digests of every batch."""
     extra = [eng.config_batch(args.config, SEED, first, n, args.align) for _ in range(FRESH_BATCHES - 1)]
     batches = [(d_arena, nbytes, d_desc)] + [(a, b, d) for a, b, d, _ in extra]
     steps = max(args.steps, 2 * FRESH_BATCHES)
@@ -797,15 +809,61 @@ def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_
         eng.update_device(a, b, d, n)
     eng.sync()
     dt = (time.perf_counter() - t0) / steps
+    ev_ms = eng.time_update_batches(batches, n, steps) / steps
     want = golden_digest(args.config, first, n)
     digests = [f"{eng.digest_device(a, b, d, n, first):016x}" for a, b, d in batches]
     for a, _, d, _ in extra:
         a.free()
         d.free()
     return {"batches": FRESH_BATCHES, "steps": steps, "value": round(frame_bytes / dt / 1e9, 2),
-            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4),
-            "frac": round(algo_bytes / dt / 1e9 / HBM_PEAK_GBS, 4), "timing": "wall clock",
+            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+            "frac": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_wall": round(algo_bytes / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "timing": "frac: HIP events around the rotated calls on the engine's stream "
+                      "(nfcs_time_update_batches); value / frac_wall: wall clock",
             "parity": None if want is None else all(g == want for g in digests)}
+
+
+def host_line(eng, args, n, reps: int = 3):
+    """The PCIe-inclusive rate (BASELINE north_star: the path starts and ends in host memory):
+    C1's frames in a host arena, nfcs_update_host (frames H2D through the NUMA-local pinned ring,
+    8-byte patch records back, applied on the host), from a pinned arena (nfcs_host_alloc) and from
+    a pageable one; wall clock per call, min and median of `reps` calls, each on freshly restored
+    frames; the digest of the result against the reference's. Never `value`."""
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(1, SEED, 0, n, args.align)
+    src = d_arena.download(np.uint8, nbytes)
+    frame_bytes = float(hdesc["len"].astype(np.float64).sum())
+    want = golden_digest(1, 0, n)
+    out = {"workload": f"C1: {human(n)} x 1500 B IPv4+UDP in host memory, nfcs_update_host "
+                       "(frames H2D, patch records D2H, applied on the host)",
+           "timing": f"wall clock per call, min / median of {reps}", "unit": "GB/s"}
+    pinned = eng.host_array(nbytes)
+    ok = True
+    try:
+        for mode, arena in (("pinned", pinned), ("pageable", np.empty(nbytes, dtype=np.uint8))):
+            arena[:] = src
+            eng.update_host(arena, hdesc, want_status=False)  # warm
+            ts = []
+            for _ in range(reps):
+                arena[:] = src
+                t0 = time.perf_counter()
+                eng.update_host(arena, hdesc, want_status=False)
+                ts.append(time.perf_counter() - t0)
+            d_arena.upload(arena)
+            got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, 0):016x}"
+            ok = ok and (want is not None and got == want)
+            ts.sort()
+            out[mode] = {"GBps": round(frame_bytes / ts[0] / 1e9, 2),
+                         "GBps_median": round(frame_bytes / ts[len(ts) // 2] / 1e9, 2),
+                         "ms_per_call": round(ts[0] * 1e3, 3), "digest": got}
+    finally:
+        eng.host_free(pinned)
+        d_arena.free()
+        d_desc.free()
+    node, local = eng.host_numa()
+    out["gpu_numa_node"], out["staging_numa_local"] = node, local
+    out["parity"] = {"reference_digest": want, "match": ok}
+    return out
 
 
 if __name__ == "__main__":

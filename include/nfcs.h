@@ -131,12 +131,18 @@ NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t 
  * a hint it is arena_bytes / n, which is exact for a batch that fills its arena and otherwise only
  * over-estimates; when that estimate says "long", the update and the L3 forward also sample the
  * frames' real footprint on the device (256 descriptors, one wave, no host sync), and the next call
- * on the same descriptor array launches in the shape the sample calls for — a burst inside a larger
+ * over the same burst (descriptor array, n and arena_bytes) launches in the shape the sample calls for — a burst inside a larger
  * ring (a NIC ring reusing its descriptor array) adapts after one call. A caller may
  * instead state its frames' mean slot size, e.g. 128 for 64-byte frames in 128-byte slots; 0 (the
  * default) restores the automatic choice. Applies to the device-path calls that follow on ctx
  * (update, L3 forward, VLAN; nfcs_update_host measures each staged chunk itself). */
 NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* ctx, uint32_t bytes);
+/* The mean footprint per packet (bytes) that the next device-path call on ctx over this burst
+ * (d_arena of arena_bytes, d_desc, n) picks its launch shape from: the slot-size hint, arena_bytes / n,
+ * or the footprint the previous call over the same burst sampled (once that call has finished).
+ * No side effect; speed only (the bytes written never depend on it). */
+NFCS_API int nfcs_ctx_launch_footprint(nfcs_ctx* ctx, uint64_t arena_bytes, const nfcs_desc* d_desc,
+                                       uint32_t n, uint64_t* mean);
 /* The host staging ring of nfcs_update_host (allocated by this call if not yet): *node = the GPU's
  * NUMA node (-1 if unknown), *local = 1 when the ring's pinned memory is bound to that node (its
  * copy threads then run on that node's CPUs). SURVEY.md §8e: one GPU per host thread, staging
@@ -314,6 +320,13 @@ NFCS_API int nfcs_stream_sync(nfcs_ctx* ctx, void* stream);
 NFCS_API int nfcs_time_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                                      const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                      int iters, void* stream, float* ms);
+/* The steady state of a NIC ring: `iters` back-to-back nfcs_update_device calls rotating over
+ * `batches` separate batches (call i runs batch i % batches: d_arenas[b], arena_bytes[b],
+ * d_descs[b], n packets each), so no call re-processes the frames the previous call wrote; HIP
+ * events on `stream` around all of them. Total milliseconds in *ms. */
+NFCS_API int nfcs_time_update_batches(nfcs_ctx* ctx, uint32_t batches, uint8_t* const* d_arenas,
+                                      const uint64_t* arena_bytes, const nfcs_desc* const* d_descs,
+                                      uint32_t n, int iters, void* stream, float* ms);
 /* Same for nfcs_flow_keys_device. */
 NFCS_API int nfcs_time_flow_keys_device(nfcs_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
                                         const nfcs_desc* d_desc, uint32_t n, nfcs_flow_key* d_keys,

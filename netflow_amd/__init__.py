@@ -62,7 +62,7 @@ KERNARG_PRELOAD = ["-mllvm", "-amdgpu-kernarg-preload-count=8"]
 
 def build(verbose: bool = False) -> str:
     """Compile the gfx950 kernels + C ABI into netflow_amd/libnfcs.so (in-tree). The measurement
-    build (extra launch forms for A/B runs) is separate: tools/exp/build.sh."""
+    build (extra launch forms for A/B runs) is separate: tools/r04/build.sh."""
     out = os.path.join(HERE, "libnfcs.so")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", *KERNARG_PRELOAD,
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc"), *SOURCES, "-o", out]
@@ -87,6 +87,7 @@ def _declare(L):
         "nfcs_ctx_destroy": ([_vp], ctypes.c_int),
         "nfcs_ctx_stream": ([_vp], _vp),
         "nfcs_ctx_set_slot_bytes": ([_vp, ctypes.c_uint32], ctypes.c_int),
+        "nfcs_ctx_launch_footprint": ([_vp, _u64, _vp, _u32, ctypes.POINTER(_u64)], ctypes.c_int),
         "nfcs_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp], ctypes.c_int),
         "nfcs_update_host": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32], ctypes.c_int),
         "nfcs_layout_config": ([ctypes.c_int, _u64, _u64, _u32, _u32, _vp, ctypes.POINTER(_u64)], ctypes.c_int),
@@ -103,6 +104,8 @@ def _declare(L):
         "nfcs_stream_sync": ([_vp, _vp], ctypes.c_int),
         "nfcs_time_update_device": ([_vp, _vp, _u64, _vp, _u32, _vp, ctypes.c_int, _vp,
                                      ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "nfcs_time_update_batches": ([_vp, _u32, _vp, _vp, _vp, _u32, ctypes.c_int, _vp,
+                                      ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "nfcs_l3_forward_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp, _vp],
                                    ctypes.c_int),
         "nfcs_vlan_device": ([_vp, _vp, _u64, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp],
@@ -238,6 +241,14 @@ class Engine:
         mean arena bytes per frame of bursts that fill only part of their arena; 0 = arena_bytes / n."""
         _check(lib().nfcs_ctx_set_slot_bytes(self.ctx, int(nbytes)), "set_slot_bytes")
 
+    def launch_footprint(self, arena_bytes: int, desc, n: int) -> int:
+        """The mean footprint per packet the next device call over this burst picks its launch
+        shape from (nfcs_ctx_launch_footprint; speed only)."""
+        m = _u64()
+        p = desc.ptr if isinstance(desc, DeviceBuffer) else int(desc)
+        _check(lib().nfcs_ctx_launch_footprint(self.ctx, arena_bytes, p, n, ctypes.byref(m)), "launch_footprint")
+        return int(m.value)
+
     def host_numa(self) -> tuple[int, bool]:
         """(NUMA node of this GPU or -1, whether the host staging ring is bound to it)."""
         node, local = ctypes.c_int(), ctypes.c_int()
@@ -368,6 +379,20 @@ class Engine:
         _check(lib().nfcs_time_update_device(self.ctx, arena.ptr, arena_bytes, desc.ptr, n,
                                              None if status is None else status.ptr, iters, stream,
                                              ctypes.byref(ms)), "time_update_device")
+        return float(ms.value)
+
+    def time_update_batches(self, batches, n, iters, stream=None) -> float:
+        """Total ms of `iters` back-to-back update_device calls rotating over `batches` — a list of
+        (arena, arena_bytes, desc), n packets each — on one stream (nfcs_time_update_batches): the
+        steady state of a NIC ring, where no call re-processes what the previous one wrote."""
+        k = len(batches)
+        p = lambda b: b.ptr if isinstance(b, DeviceBuffer) else int(b)
+        arenas = (_vp * k)(*[p(a) for a, _, _ in batches])
+        sizes = (_u64 * k)(*[int(nb) for _, nb, _ in batches])
+        descs = (_vp * k)(*[p(d) for _, _, d in batches])
+        ms = ctypes.c_float()
+        _check(lib().nfcs_time_update_batches(self.ctx, k, arenas, sizes, descs, n, iters, stream,
+                                              ctypes.byref(ms)), "time_update_batches")
         return float(ms.value)
 
     # ---- synthetic batches / digests ----------------------------------------------------

@@ -72,7 +72,9 @@ struct nfcs_ctx {
     // descriptor array it belongs to
     uint32_t* obs_host = nullptr;
     uint32_t* obs_dev = nullptr;
-    const void* obs_desc = nullptr;
+    const void* obs_desc = nullptr;  // the sampled call: descriptor array, burst size and arena
+    uint32_t obs_n = 0;
+    uint64_t obs_bytes = 0;
 };
 
 namespace {
@@ -404,17 +406,32 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
 // result), and the next call on the same descriptor array launches in the shape that sample says:
 // a NIC ring reusing its descriptor array adapts after one call, with no hint and no host sync.
 struct Shape { uint64_t mean; uint32_t* obs; };
-Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
+// The shape a call over this burst launches in, without side effects (nfcs_ctx_launch_footprint):
+// `fresh` = the burst differs from the sampled one, so the call samples anew.
+Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, bool* fresh) {
+    *fresh = false;
     if (c->slot_bytes) return {c->slot_bytes, nullptr};
+    if (n == 0) return {arena_bytes, nullptr};  // nothing is launched; never divide by zero
     const uint64_t est = arena_bytes / n;
     if (est < nfcs::kSmallMeanBytes || !c->obs_host) return {est, nullptr};
-    if (c->obs_desc != d_desc) {  // another descriptor array: its own observation, from this call on
-        c->obs_desc = d_desc;
-        __atomic_store_n(c->obs_host, 0u, __ATOMIC_RELAXED);
+    if (c->obs_desc != d_desc || c->obs_n != n || c->obs_bytes != arena_bytes) {
+        // another burst (descriptor array, size or arena): its own observation, from this call on
+        *fresh = true;
         return {est, c->obs_dev};
     }
     const uint32_t o = __atomic_load_n(c->obs_host, __ATOMIC_RELAXED);  // the latest call's sample
     return {o ? std::min<uint64_t>(o, est) : est, c->obs_dev};
+}
+Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
+    bool fresh = false;
+    const Shape sh = peek_shape(c, arena_bytes, d_desc, n, &fresh);
+    if (fresh) {
+        c->obs_desc = d_desc;
+        c->obs_n = n;
+        c->obs_bytes = arena_bytes;
+        __atomic_store_n(c->obs_host, 0u, __ATOMIC_RELAXED);
+    }
+    return sh;
 }
 
 // The device-resident update on stream st: kUpdateAuto, deferred records into the caller's
@@ -520,6 +537,14 @@ NFCS_API void* nfcs_ctx_stream(nfcs_ctx* c) { return c ? (void*)c->stream : null
 NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* c, uint32_t bytes) {
     if (!c) return NFCS_EINVAL;
     c->slot_bytes = bytes;
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_ctx_launch_footprint(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
+                                       uint32_t n, uint64_t* mean) {
+    if (!c || !mean) return NFCS_EINVAL;
+    bool fresh = false;
+    *mean = peek_shape(c, arena_bytes, d_desc, n, &fresh).mean;
     return NFCS_OK;
 }
 
@@ -865,6 +890,27 @@ NFCS_API int nfcs_time_update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t are
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it) {
         const int rc = update_device(c, d_arena, arena_bytes, d_desc, n, d_status, nullptr, st);
+        if (rc) return rc;
+    }
+    NFCS_HIP(hipEventRecord(c->ev1, st));
+    NFCS_HIP(hipEventSynchronize(c->ev1));
+    NFCS_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_time_update_batches(nfcs_ctx* c, uint32_t batches, uint8_t* const* d_arenas,
+                                      const uint64_t* arena_bytes, const nfcs_desc* const* d_descs,
+                                      uint32_t n, int iters, void* stream, float* ms) {
+    if (!c || !ms || iters <= 0 || batches == 0 || !d_arenas || !arena_bytes || !d_descs) return NFCS_EINVAL;
+    for (uint32_t b = 0; b < batches; ++b)
+        if (!d_arenas[b] || !d_descs[b] || ((uintptr_t)d_arenas[b] & 15u)) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
+    hipStream_t st = pick(c, stream);
+    NFCS_HIP(hipEventRecord(c->ev0, st));
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t b = (uint32_t)it % batches;
+        const int rc = update_device(c, d_arenas[b], arena_bytes[b], d_descs[b], n, nullptr, nullptr, st);
         if (rc) return rc;
     }
     NFCS_HIP(hipEventRecord(c->ev1, st));

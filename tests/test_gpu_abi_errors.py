@@ -149,3 +149,43 @@ def test_stream_read_reference(engine):
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 6, 1, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, d.ptr, 4096, 0, 0, None, ctypes.byref(ms)) == EINVAL
     assert L.nfcs_time_stream_read(engine.ctx, None, 4096, 0, 1, None, ctypes.byref(ms)) == EINVAL
+
+
+def test_timing_entries_with_no_packets(engine):
+    """the time_* entry points reach the launch-shape choice, which divided the arena size
+    by n: with n = 0 and no slot hint every one of them is a clean no-op (NFCS_OK, ~0 ms)."""
+    L = nf.lib()
+    d = engine.alloc(4096)
+    ms = ctypes.c_float()
+    engine.set_slot_bytes(0)
+    assert L.nfcs_time_update_device(engine.ctx, d.ptr, 4096, d.ptr, 0, None, 2, None, ctypes.byref(ms)) == OK
+    assert L.nfcs_time_l3_forward_device(engine.ctx, d.ptr, 4096, d.ptr, d.ptr, 0, d.ptr, 1, None, 2, None,
+                                         ctypes.byref(ms)) == OK
+    assert L.nfcs_time_vlan_device(engine.ctx, d.ptr, 4096, d.ptr, 0, 0, 0, 1536, None, 2, None,
+                                   ctypes.byref(ms)) == OK
+    assert L.nfcs_time_flow_keys_device(engine.ctx, d.ptr, 4096, d.ptr, 0, d.ptr, None, 2, None,
+                                        ctypes.byref(ms)) == OK
+    arenas = (ctypes.c_void_p * 1)(d.ptr)
+    sizes = (ctypes.c_uint64 * 1)(4096)
+    assert L.nfcs_time_update_batches(engine.ctx, 1, arenas, sizes, arenas, 0, 2, None, ctypes.byref(ms)) == OK
+    assert engine.launch_footprint(4096, d, 0) == 4096
+    # and the rotation's own argument rules
+    assert L.nfcs_time_update_batches(engine.ctx, 0, arenas, sizes, arenas, 0, 2, None, ctypes.byref(ms)) == EINVAL
+    bad = (ctypes.c_void_p * 1)(d.ptr + 8)
+    assert L.nfcs_time_update_batches(engine.ctx, 1, bad, sizes, arenas, 1, 2, None, ctypes.byref(ms)) == EINVAL
+
+
+def test_rotating_timing_matches_the_reference(engine):
+    """nfcs_time_update_batches (bench.py's `fresh` sub-line): rotating over 3 batches of fuzz frames,
+    every batch ends equal to the oracle's update of it."""
+    bs, refs = [], []
+    for k in range(3):
+        arena, desc = oracle.pack_frames(oracle.fuzz_frames(600 + k, 0, 3000))
+        ref = arena.copy()
+        oracle.update_batch(ref, desc)
+        bs.append((engine.alloc(arena.nbytes).upload(arena), arena.nbytes, engine.alloc(desc.nbytes).upload(desc)))
+        refs.append(ref)
+    n = 3000
+    assert engine.time_update_batches(bs, n, 7) > 0
+    for (a, nb, _), ref in zip(bs, refs):
+        assert np.array_equal(a.download(np.uint8, nb), ref)

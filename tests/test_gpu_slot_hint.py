@@ -111,9 +111,10 @@ def ring_burst(n, L, slot, seed):
 def test_ring_burst_adapts_without_hint(engine):
     """1M 64-byte frames at the start of a 4 GiB ring, NO slot-size hint: arena_bytes / n (4 KiB)
     says long frames, so the first call runs the long shape and samples the frames' footprint
-    (sample_footprint); from the second call on the same descriptor array the launch runs the shape
-    the sample calls for (8-lane rows), as fast as with the hint. Bytes equal the oracle's at every
-    call (the shape picks speed only)."""
+    (sample_footprint); from the second call over the same burst the launch runs the shape the
+    sample calls for (8-lane rows below kTinyMeanBytes = 800). The shape is read back directly
+    (nfcs_ctx_launch_footprint), not inferred from timings; bytes equal the oracle's at every call
+    (the shape picks speed only). The times are printed for the record, never asserted."""
     n, L, slot, ring = 1 << 20, 64, 128, 4 << 30
     host, desc = ring_burst(n, L, slot, 7)
     ref = host.copy()
@@ -123,23 +124,29 @@ def test_ring_burst_adapts_without_hint(engine):
     d = engine.alloc(desc.nbytes).upload(desc)
     try:
         a.upload(host)
+        assert engine.launch_footprint(ring, d, n) == ring // n  # nothing sampled yet: the long shape
         first = engine.time_update_device(a, ring, d, n, 1)  # the long shape + the sample
         engine.sync()
         assert np.array_equal(a.download(np.uint8, host.nbytes), ref)
+        fp = engine.launch_footprint(ring, d, n)
+        assert fp < 800 and fp >= slot, fp  # the sample: 128-byte slots -> 8-lane rows from now on
+        assert engine.launch_footprint(ring, d, n - 4) == ring // (n - 4)  # another burst: not its sample
         engine.time_update_device(a, ring, d, n, 10)  # warm
         adapted = engine.time_update_device(a, ring, d, n, 40) / 40
         assert np.array_equal(a.download(np.uint8, host.nbytes), ref)  # idempotent
         engine.set_slot_bytes(slot)
+        assert engine.launch_footprint(ring, d, n) == slot
         engine.time_update_device(a, ring, d, n, 10)
         hinted = engine.time_update_device(a, ring, d, n, 40) / 40
         print(f"1M x 64 B in a 4 GiB ring: first call {first * 1e3:.1f} us, adapted {adapted * 1e3:.1f} us, "
               f"with the hint {hinted * 1e3:.1f} us")
-        assert adapted < 1.15 * hinted + 0.005  # ms
         # VLAN push/pop on the same ring adapts the same way (its kernel samples too); an even
         # number of alternating push / pop calls leaves every frame as it was
         engine.set_slot_bytes(0)
         push = nf.vlan_push_op(100, 3)
         vfirst = engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 2)
+        fp = engine.launch_footprint(ring, d, n)
+        assert fp < 800 and fp >= slot, fp
         engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 10)
         vadapted = engine.time_vlan_device(a, ring, d, n, push, nf.VLAN_POP, slot, 40) / 40
         engine.set_slot_bytes(slot)
@@ -151,7 +158,6 @@ def test_ring_burst_adapts_without_hint(engine):
         assert np.array_equal(got[:, :L], ref.reshape(n, slot)[:, :L])
         print(f"VLAN push/pop: first pair {vfirst / 2 * 1e3:.1f} us per call, adapted {vadapted * 1e3:.1f} us, "
               f"with the hint {vhinted * 1e3:.1f} us")
-        assert vadapted < 1.15 * vhinted + 0.005  # ms
     finally:
         engine.set_slot_bytes(0)
         a.free()

@@ -3,7 +3,7 @@ literal text substitutions in the sources under netflow_amd/csrc (nfcs_kernels.h
 nfcs_internal.h; each OLD must occur exactly COUNT times over them, default 1; the patched copies are
 compiled together from one scratch directory, so a quoted #include finds the patched header),
 so a one-line policy or shape change can be A/B-timed against the product without touching it:
-  python tools/exp/patch_build.py OUT.so 'OLD' 'NEW' ['OLD' 'NEW' ...]
+  python tools/patch_build.py OUT.so 'OLD' 'NEW' ['OLD' 'NEW' ...]
   NFCS_LIB=OUT.so python bench.py --op flowkey --no-cpu
 Prefix OLD with '<N>*' to require N occurrences (all replaced)."""
 import os
@@ -11,7 +11,7 @@ import subprocess
 import sys
 import tempfile
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():

@@ -1,0 +1,152 @@
+// fresh_exp.hip — round-4 measurement translation unit (not product). Built with nfcs_api.hip into
+// tools/r04/libnfcs_r4.so by tools/r04/build.sh; the product library never contains it.
+//
+// It compiles the product kernels (the text of netflow_amd/csrc/nfcs_kernels.hip) and adds launch
+// forms for the question VERDICT r3 item 1 asks: where a C1 call over a batch that the previous call
+// did NOT touch (a NIC ring's steady state) loses its time, and which way of writing the 2+2
+// checksum bytes costs least there. Variants (long shape, 256-thread workgroups, line-aligned rows):
+//   0   the product (launch_update, kUpdateAuto)
+//   1   read pass writing patch records only, frames untouched (the floor: no frame writes)
+//   2/3 the product's read pass + its write pass with write-back / write-through (sc1) byte stores
+//   4/5/6 read pass storing each frame's first 64 bytes whole, past the caches / write-through /
+//       write-back (SF_SECTOR_*), no write pass
+//   7/8 the product's read pass + a write pass that re-reads each deferred frame's first 64 bytes and
+//       stores them whole with the bytes patched in, past the caches / write-through
+//   9   every wave inline (SF_INLINE: byte stores, sc1), no write pass
+//  10   the product in 512K-packet sub-batches (its form above 1M packets) at any n
+#include "../../netflow_amd/csrc/nfcs_kernels.hip"
+
+namespace nfcs {
+
+template <int POL>  // 0 write-back, 1 write-through (sc1), 2 past the caches (sc0 sc1 nt)
+DEV void xst8(uint8_t* p, uint32_t b) {
+    if (POL == 0) *p = (uint8_t)b;
+    else if (POL == 1) __hip_atomic_store(p, (uint8_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else st8_nt(p, b);
+}
+
+// apply_bytes_kernel with the store policy as a parameter
+template <int POL>
+__global__ __launch_bounds__(kBlock) void apply_bytes_pol_kernel(uint8_t* __restrict__ arena,
+                                                                 const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                                 uint32_t base16, const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
+    uint2 r0 = make_uint2(0u, 0u);
+    if (i < n) r0 = ((const uint2*)rec)[i];
+    uint32_t s = defer_len(d.len);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);
+    s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);
+    const bool dfr = i < n && defer_group(s, 4);
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(dfr);
+    if (!mask) return;
+    const uint2 r = dfr ? r0 : make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
+    const uint32_t j = lane & 3u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (((mask >> (16u * k)) & 0xFFFFu) == 0) continue;
+        const int q4 = (int)((16u * k + (lane >> 2)) * 4u);
+        const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.x);
+        const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.y);
+        const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d.off16);
+        const uint32_t ipo = rx & 0xFFFFu, l4o = rx >> 16;
+        const uint32_t off = j < 2 ? ipo : l4o;
+        const uint32_t a = off + (j & 1u);
+        const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+        if (off != NFCS_PATCH_NONE && !overlap) {
+            const uint32_t b = (j < 2 ? (ry >> (8 * j)) : (ry >> (16 + 8 * (j - 2)))) & 0xFFu;
+            xst8<POL>(arena + ((uint64_t)o16 - base16) * 16u + a, b);
+        }
+    }
+}
+
+// Write pass storing each deferred frame's first 64 bytes whole: 4 lanes per packet (lane j: frame
+// chunk j), 64 packets per workgroup; the chunk is re-read (default policy), the fields patched in
+// (IPv4 first, then L4, as the reference writes them) and stored back. Frames whose fields lie past
+// byte 63, or shorter than 64 bytes, get byte stores.
+template <int POL>  // 1 write-through (sc1), 2 past the caches
+__global__ __launch_bounds__(kBlock) void apply_sector_kernel(uint8_t* __restrict__ arena,
+                                                              const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                              uint32_t base16, const nfcs_patch* __restrict__ rec) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t p = t >> 2;
+    const uint32_t j = (uint32_t)t & 3u;
+    if (p >= n) return;
+    const uint64_t q0 = p & ~3ull;
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) s += (q0 + i < n) ? defer_len(desc[q0 + i].len) : 0u;
+    if (!defer_group(s, 4)) return;
+    const nfcs_desc d = desc[p];
+    const uint2 r = ((const uint2*)rec)[p];
+    const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
+    if (ipo == NFCS_PATCH_NONE && l4o == NFCS_PATCH_NONE) return;
+    const uint32_t ipw = ipo | ((r.y & 0xFFFFu) << 16), l4w = l4o | (r.y & 0xFFFF0000u);
+    uint8_t* f = arena + ((uint64_t)d.off16 - base16) * 16u;
+    const bool sec = d.len >= 64u && (ipo == NFCS_PATCH_NONE || ipo < 63u) && (l4o == NFCS_PATCH_NONE || l4o < 63u);
+    if (sec) {
+        const uint4 v = put_field(put_field(((const uint4*)f)[j], ipw, j), l4w, j);
+        if (POL == 2) st16_nt((uint4*)f + j, v);
+        else st16<true>((uint4*)f + j, v);
+        return;
+    }
+    const uint32_t off = j < 2 ? ipo : l4o;
+    const uint32_t a = off + (j & 1u);
+    const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+    if (off != NFCS_PATCH_NONE && !overlap)
+        st8_nt(f + a, (j < 2 ? (r.y >> (8 * j)) : (r.y >> (16 + 8 * (j - 2)))) & 0xFFu);
+}
+
+static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_desc* desc, uint32_t n,
+                            nfcs_patch* ws, hipStream_t st) {
+    const FwdArgs nofwd = {nullptr, nullptr, 0, nullptr};
+    const uint32_t g4 = (n + 15u) / 16u, gb = (n + kBlock - 1) / kBlock, gs = (uint32_t)(((uint64_t)n * 4 + kBlock - 1) / kBlock);
+#define ROWS(SF) launch_rows<6, 16, 1, kBlock, false, SF, 1, 7>(g4, kRowsLdsPad, st, arena, bytes, desc, n, 0u, nullptr, \
+                                                               (SF == SF_RECORDS) ? ws : nullptr, ws, nofwd)
+    switch (v) {
+    case 0: return launch_update(DevInfo{}, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, kUpdateAuto, st);
+    case 1: ROWS(SF_RECORDS); break;
+    case 2: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_bytes_pol_kernel<0>, dim3(gb), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
+    case 3: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_bytes_pol_kernel<1>, dim3(gb), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
+    case 4: ROWS(SF_SECTOR_NT); break;
+    case 5: ROWS(SF_SECTOR_WT); break;
+    case 6: ROWS(SF_SECTOR_WB); break;
+    case 7: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_sector_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
+    case 8: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_sector_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
+    case 9: ROWS(SF_INLINE); break;
+    case 10:
+        for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
+            const hipError_t e = launch_update(DevInfo{}, arena, bytes, desc + i, std::min(kSubBatchPackets, n - i), 0u,
+                                               nullptr, nullptr, ws, kUpdateAuto, st);
+            if (e != hipSuccess) return e;
+        }
+        break;
+    default: return hipErrorInvalidValue;
+    }
+#undef ROWS
+    return hipGetLastError();
+}
+
+}  // namespace nfcs
+
+// `iters` back-to-back launches of variant v rotating over `batches` batches (call i: batch i %
+// batches), HIP events on `stream` around them; ws: 8 bytes per packet. Total ms in *ms.
+extern "C" NFCS_API int nfcs_r4_time(int v, uint32_t batches, uint8_t* const* arenas, const uint64_t* bytes,
+                                     const nfcs_desc* const* descs, uint32_t n, nfcs_patch* ws, int iters,
+                                     void* stream, float* ms) {
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1;
+    hipError_t e = hipEventRecord(e0, st);
+    for (int it = 0; it < iters && e == hipSuccess; ++it) {
+        const uint32_t b = (uint32_t)it % batches;
+        e = nfcs::r4_launch(v, arenas[b], bytes[b], descs[b], n, ws, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return (int)e;
+}
