@@ -799,9 +799,16 @@ def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_
     extra = [eng.config_batch(args.config, SEED, first, n, args.align) for _ in range(FRESH_BATCHES - 1)]
     batches = [(d_arena, nbytes, d_desc)] + [(a, b, d) for a, b, d, _ in extra]
     steps = max(args.steps, 2 * FRESH_BATCHES)
-    for k in range(2 * FRESH_BATCHES):  # warm
+    # warm-up as for the main line (the batches were generated with the GPU idle between host
+    # steps; its clock takes tens of ms of load to come back: a rocprofv3 trace of the rotation
+    # shows the read pass at 260 -> 246 -> 233 -> 229 us over its first 100 calls)
+    tw, k = time.perf_counter(), 0
+    while k < 2 * FRESH_BATCHES or time.perf_counter() - tw < args.warm_seconds:
         a, b, d = batches[k % FRESH_BATCHES]
         eng.update_device(a, b, d, n)
+        k += 1
+        if k % 16 == 0:
+            eng.sync()
     eng.sync()
     t0 = time.perf_counter()
     for k in range(steps):

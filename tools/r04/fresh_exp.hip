@@ -14,6 +14,17 @@
 //       stores them whole with the bytes patched in, past the caches / write-through
 //   9   every wave inline (SF_INLINE: byte stores, sc1), no write pass
 //  10   the product in 512K-packet sub-batches (its form above 1M packets) at any n
+//  11/12/13 the short shape (16-lane rows, one-wave workgroups at 7 waves/SIMD, C3's) storing each
+//       frame's first 64 bytes whole past the caches / write-through / write-back
+//  14   the short shape with its inline byte stores (the product's form for C3)
+//  15   the short shape writing patch records only (C3's read floor in its own shape; no parity)
+//  30/31/32 every wave defers (SF_REC64, long shape): 64-byte header records + a write pass that
+//       stores each frame's first 64 bytes whole from them, past the caches / write-through / write-back
+//  33/34 the same in the short shape (C3's), past the caches / write-through
+// Timing-only bounds (they write placeholder bytes: no parity):
+//  20   the read pass's loads alone (launch_frames_read: nothing computed or written)
+//  21   writes alone: 4 byte stores per packet at frame bytes 24, 25, 40, 41 (sc0 sc1 nt), no reads
+//  22/23 writes alone: each frame's first 64 bytes stored whole, past the caches / write-through
 #include "../../netflow_amd/csrc/nfcs_kernels.hip"
 
 namespace nfcs {
@@ -98,12 +109,57 @@ __global__ __launch_bounds__(kBlock) void apply_sector_kernel(uint8_t* __restric
         st8_nt(f + a, (j < 2 ? (r.y >> (8 * j)) : (r.y >> (16 + 8 * (j - 2)))) & 0xFFu);
 }
 
+// Timing-only write bounds (variants 21-23): 4 lanes per packet, no frame reads.
+template <int FORM>  // 0 four bytes (nt), 1 64-byte sector (nt), 2 64-byte sector (sc1)
+__global__ __launch_bounds__(kBlock) void write_only_kernel(uint8_t* __restrict__ arena,
+                                                            const nfcs_desc* __restrict__ desc, uint32_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t p = t >> 2;
+    const uint32_t j = (uint32_t)t & 3u;
+    if (p >= n) return;
+    const nfcs_desc d = desc[p];
+    uint8_t* f = arena + (uint64_t)d.off16 * 16u;
+    if (d.len < 64u) return;
+    if (FORM == 0) st8_nt(f + (j < 2 ? 24u + j : 38u + j), 0x5Au);
+    else if (FORM == 1) st16_nt((uint4*)f + j, make_uint4(j, 1u, 2u, 3u));
+    else st16<true>((uint4*)f + j, make_uint4(j, 1u, 2u, 3u));
+}
+
+// SF_REC64's write pass: 4 lanes per packet; a flagged packet's 64-byte record (dense, coalesced)
+// goes into its frame's first 64 bytes whole, other records as byte stores.
+template <int POL>  // 0 write-back, 1 write-through (sc1), 2 past the caches
+__global__ __launch_bounds__(kBlock) void apply_rec64_kernel(uint8_t* __restrict__ arena,
+                                                             const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                             const nfcs_patch* __restrict__ rec) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t p = t >> 2;
+    const uint32_t j = (uint32_t)t & 3u;
+    if (p >= n) return;
+    const nfcs_desc d = desc[p];
+    const uint2 r = ((const uint2*)rec)[p];
+    uint8_t* f = arena + (uint64_t)d.off16 * 16u;
+    if (r.x == kRec64Flag) {
+        const uint4 v = ((const uint4*)(rec + kRec64Records))[p * 4u + j];
+        if (POL == 2) st16_nt((uint4*)f + j, v);
+        else st16<POL == 1>((uint4*)f + j, v);
+        return;
+    }
+    const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
+    const uint32_t off = j < 2 ? ipo : l4o;
+    const uint32_t a = off + (j & 1u);
+    const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+    if (off != NFCS_PATCH_NONE && !overlap)
+        st8_nt(f + a, (j < 2 ? (r.y >> (8 * j)) : (r.y >> (16 + 8 * (j - 2)))) & 0xFFu);
+}
+
 static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_desc* desc, uint32_t n,
                             nfcs_patch* ws, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0, nullptr};
     const uint32_t g4 = (n + 15u) / 16u, gb = (n + kBlock - 1) / kBlock, gs = (uint32_t)(((uint64_t)n * 4 + kBlock - 1) / kBlock);
 #define ROWS(SF) launch_rows<6, 16, 1, kBlock, false, SF, 1, 7>(g4, kRowsLdsPad, st, arena, bytes, desc, n, 0u, nullptr, \
                                                                (SF == SF_RECORDS) ? ws : nullptr, ws, nofwd)
+#define SHORT(SF) launch_rows<6, 16, 7, 64, false, SF, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, \
+                                                           nullptr, ws, nofwd)
     switch (v) {
     case 0: return launch_update(DevInfo{}, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, kUpdateAuto, st);
     case 1: ROWS(SF_RECORDS); break;
@@ -122,9 +178,29 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
             if (e != hipSuccess) return e;
         }
         break;
+    case 11: SHORT(SF_SECTOR_NT); break;
+    case 12: SHORT(SF_SECTOR_WT); break;
+    case 13: SHORT(SF_SECTOR_WB); break;
+    case 14: SHORT(SF_INLINE); break;
+    case 15: launch_rows<6, 16, 7, 64, false, SF_RECORDS, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr,
+                                                              ws, ws, nofwd); break;
+    case 30: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 31: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 32: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<0>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 33: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 34: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 20: {
+        static unsigned long long* sink = nullptr;
+        if (!sink && hipMalloc(&sink, 64) != hipSuccess) return hipErrorOutOfMemory;
+        return launch_frames_read(arena, bytes, desc, n, sink, st);
+    }
+    case 21: hipLaunchKernelGGL(write_only_kernel<0>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n); break;
+    case 22: hipLaunchKernelGGL(write_only_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n); break;
+    case 23: hipLaunchKernelGGL(write_only_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n); break;
     default: return hipErrorInvalidValue;
     }
 #undef ROWS
+#undef SHORT
     return hipGetLastError();
 }
 

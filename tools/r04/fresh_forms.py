@@ -50,7 +50,7 @@ def main():
     for w in a.work.split(","):
         cfg, n = WORK[w]
         bs = [eng.config_batch(cfg, SEED, 0, n, 128) for _ in range(a.batches)]
-        ws = eng.alloc(8 * n)
+        ws = eng.alloc(8 * (1 << 22) + 64 * n)  # 8-byte records, then SF_REC64's 64-byte ones
         algo = float(bs[0][3]["len"].astype("f8").sum()) + 12.0 * n
         want = golden(cfg, 0, n)
 
