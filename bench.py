@@ -10,9 +10,11 @@ already resident in HBM.
                   [--op update|l3fwd|flowkey|vlan] [--strong]
 
 Workloads (BASELINE.json configs):
-  N = 1   config C1: 1M x 1500 B IPv4+UDP (configs[1]); the line also carries a `fresh` sub-line —
-          the same work rotated over 4 separately generated batches, so no launch re-processes
-          what the previous one just wrote (a NIC ring's steady state).
+  N = 1   config C1: 1M x 1500 B IPv4+UDP (configs[1]). The timed calls rotate over 4 separately
+          generated batches (2 above 1M packets), so no call re-processes what the previous one just
+          wrote (a NIC ring's steady state; --batches 1 replays one batch). The line also carries the
+          one-batch `replay` sub-line, the `c4_shard` sub-line (the per-GPU batch of N > 1) and the
+          `host` sub-line (the same frames in host memory through nfcs_update_host, PCIe included).
   N > 1   config C4: 32M x 1500 B sharded as independent 4M-packet batches, one per GPU (also at 2
           and 4 GPUs): per-GPU work fixed, scaling "weak". `--strong` instead splits ONE batch of
           the config's size across the ranks by bytes (nfcs_shard_bytes; e.g. the mixed C3), whose
@@ -413,7 +415,10 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch sub-line")
+    ap.add_argument("--batches", type=int, default=0,
+                    help="update: batches the timed calls rotate over (default 4 up to 1M packets, 2 "
+                         "above; 1 = replay one batch)")
+    ap.add_argument("--no-replay", action="store_true", help="skip the one-batch replay sub-line")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the C4-shard sub-line")
     ap.add_argument("--no-host", action="store_true", help="N = 1: skip the host-memory (PCIe) sub-line")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
@@ -505,7 +510,20 @@ def main():
         algo_bytes = 2.0 * frame_bytes + 4.0 * n + 12.0 * n
         regen = lambda: step() if flip[0] else None  # back to untagged frames (pop)
     else:
-        step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
+        # The steady state of a NIC ring: the calls rotate over `nrot`
+        # separately generated batches, so no call re-processes what the previous call wrote and
+        # no header line is still in the memory-side cache from an earlier pass over the same
+        # frames. 4 batches up to 1M packets (4 x 128 MB of header lines > the 256 MB Infinity
+        # Cache), 2 above (a 4M batch alone is 25x the cache). --batches 1 replays one batch.
+        nrot = args.batches or (FRESH_BATCHES if n <= (1 << 20) else 2)
+        extra = [eng.config_batch(args.config, SEED, first, n, args.align)[:3] for _ in range(nrot - 1)]
+        batches = [(d_arena, nbytes, d_desc)] + extra
+        ctr = [0]
+
+        def step():
+            a, b, d = batches[ctr[0] % nrot]
+            ctr[0] += 1
+            eng.update_device(a, b, d, n)
         regen = lambda: None
 
     # torch (for the synchronize around the timed region) was initialised before the engine
@@ -588,14 +606,20 @@ def main():
                           "frac_is_on": "min(len, 128): the frame's first 128-byte line, the two 64-byte "
                                         "sectors the 82 header bytes span"}
     else:
-        ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, args.steps) / args.steps
+        # the same rotation, HIP events on the engine's stream around all the calls
+        ev_ms = eng.time_update_batches(batches, n, args.steps) / args.steps
         # SURVEY.md §8d asks for the median of >= 20 reps: each call timed alone by its own events
-        single = sorted(eng.time_update_device(d_arena, nbytes, d_desc, n, 1) for _ in range(max(args.steps, 20)))
+        # (batch k % nrot, so each still runs over frames the previous call did not touch)
+        single = sorted(eng.time_update_device(*batches[k % nrot][:2], batches[k % nrot][2], n, 1)
+                        for k in range(max(args.steps, 20)))
         extra_roofline = {"kernel_ms_median_single": round(single[len(single) // 2], 4),
                           "kernel_ms_min_single": round(single[0], 4),
-                          "single_reps": len(single)}
-        # parity of what was measured: digest of the updated arena vs the reference's
+                          "single_reps": len(single),
+                          "batches_rotated": nrot}
+        # parity of what was measured: digest of every updated batch vs the reference's
         want = golden_digest(args.config, first, n)
+        digests = [f"{eng.digest_device(a, b, d, n, first):016x}" for a, b, d in batches]
+        got = digests[0] if len(set(digests)) == 1 else "batches differ: " + ",".join(digests)
     achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
     if got is None:
         got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
@@ -611,9 +635,13 @@ def main():
         parity_ok = parity["match"]
     parity["all_ranks"] = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
-    fresh = None
-    if ws == 1 and args.op == "update" and not args.no_fresh and args.config in (1, 2, 3):
-        fresh = fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc)
+    replay = None
+    if args.op == "update":
+        for a, _, d in batches[1:]:
+            a.free()
+            d.free()
+        if ws == 1 and not args.no_replay and nrot > 1:
+            replay = replay_line(eng, args, first, n, algo_bytes, d_arena, nbytes, d_desc)
 
     traffic = load_traffic(args.config, n, args.op) if args.align == 128 else None
     # N = 1: the C4 shard (4M x 1500 B, the per-GPU batch of the N > 1 lines) as a sub-line, so the
@@ -699,8 +727,8 @@ def main():
                                            f"{nbytes / 1e9:.3f} GB arena (arena bytes per time) and "
                                            "nfcs_time_frames_read over its frames (frame + descriptor bytes per time)",
                                  "round1_microbench_GBps": STREAM_READ_GBPS}
-    if fresh is not None:
-        out["fresh"] = fresh
+    if replay is not None:
+        out["replay"] = replay
     if c4_wanted:
         d_arena.free()
         d_arena = None
@@ -757,14 +785,21 @@ def timed_steps(eng, step, steps: int, regen=None) -> float:
 
 def c4_shard_line(eng, args):
     """BASELINE C4's per-GPU batch — rank 0's shard, packets [0, 4M) of the 1500-byte stream —
-    on this one GPU: warm-up, wall clock over the steps, the kernels' HIP-event time, the
-    reference's digest of that shard (configs.json c4_rank_shards)."""
+    on this one GPU, as the N > 1 lines run it: calls rotating over 2 separately generated shards
+    (the steady state), warm-up, wall clock over the steps, the rotation's HIP-event time, the
+    reference's digest of that shard (configs.json c4_rank_shards) for both copies."""
     n = C4_PACKETS_PER_GPU
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(1, SEED, 0, n, args.align)
+    batches = [(d_arena, nbytes, d_desc), eng.config_batch(1, SEED, 0, n, args.align)[:3]]
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n
-    step = lambda: eng.update_device(d_arena, nbytes, d_desc, n)
-    steps = max(args.steps // 4, 5)
+    ctr = [0]
+
+    def step():
+        a, b, d = batches[ctr[0] % 2]
+        ctr[0] += 1
+        eng.update_device(a, b, d, n)
+    steps = max(args.steps // 4, 6)
     tw = time.perf_counter()
     done = 0
     while done < args.warmup or time.perf_counter() - tw < 0.3:
@@ -772,63 +807,51 @@ def c4_shard_line(eng, args):
         done += 1
     eng.sync()
     dt = timed_steps(eng, step, steps) / steps
-    ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, steps) / steps
+    ev_ms = eng.time_update_batches(batches, n, steps) / steps
     # the read-only floor of the same frames in the read pass's pattern, and the best buffer stream
     rd_ms = eng.time_frames_read(d_arena, nbytes, d_desc, n, steps) / steps
     st_ms = eng.time_stream_read(d_arena, nbytes, steps, form=5) / steps
     ceil = max((frame_bytes + 8.0 * n) / (rd_ms * 1e-3) / 1e9, nbytes / (st_ms * 1e-3) / 1e9)
     want = golden_digest(1, 0, n)
-    got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, 0):016x}"
-    d_arena.free()
-    d_desc.free()
+    digests = [f"{eng.digest_device(a, b, d, n, 0):016x}" for a, b, d in batches]
+    got = digests[0] if len(set(digests)) == 1 else "batches differ: " + ",".join(digests)
+    for a, _, d in batches:
+        a.free()
+        d.free()
     return {"workload": "C4 shard: rank 0's 4M x 1500 B IPv4+UDP (the per-GPU batch of the N > 1 lines)",
-            "packets": n, "steps": steps, "value": round(frame_bytes / dt / 1e9, 2), "unit": "GB/s",
-            "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+            "packets": n, "steps": steps, "batches_rotated": 2, "value": round(frame_bytes / dt / 1e9, 2),
+            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
             "frac": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "read_only_GBps": round(ceil, 1),
             "frac_of_read_only": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / ceil, 4),
             "parity": {"digest": got, "reference_digest": want, "match": None if want is None else got == want}}
 
 
-def fresh_line(eng, args, first, n, frame_bytes, algo_bytes, d_arena, nbytes, d_desc):
-    """The steady state of a NIC ring: the same work rotated over FRESH_BATCHES separately generated
-    batches (the timed one plus FRESH_BATCHES - 1 more), so no call runs over what the previous call
-    just wrote and no header line is still in the memory-side cache from a previous pass over the
-    same batch. Wall clock around the steps, then the same rotation timed by HIP events on the
-    engine's stream (nfcs_time_update_batches: `frac`), then digests of every batch."""
-    extra = [eng.config_batch(args.config, SEED, first, n, args.align) for _ in range(FRESH_BATCHES - 1)]
-    batches = [(d_arena, nbytes, d_desc)] + [(a, b, d) for a, b, d, _ in extra]
-    steps = max(args.steps, 2 * FRESH_BATCHES)
-    # warm-up as for the main line (the batches were generated with the GPU idle between host
-    # steps; its clock takes tens of ms of load to come back: a rocprofv3 trace of the rotation
-    # shows the read pass at 260 -> 246 -> 233 -> 229 us over its first 100 calls)
+def replay_line(eng, args, first, n, algo_bytes, d_arena, nbytes, d_desc):
+    """The same work REPLAYED on one batch (every call re-processes the frames the previous call
+    wrote: their header lines are still in the memory-side cache, and the previous call's dirty
+    lines are rewritten there instead of being written back to HBM) — the rounds 1-3 headline form,
+    kept beside the steady-state rotation for comparison. Wall clock and HIP events; digest."""
+    steps = max(args.steps, 8)
     tw, k = time.perf_counter(), 0
-    while k < 2 * FRESH_BATCHES or time.perf_counter() - tw < args.warm_seconds:
-        a, b, d = batches[k % FRESH_BATCHES]
-        eng.update_device(a, b, d, n)
+    while k < 8 or time.perf_counter() - tw < args.warm_seconds:  # warm as the main line
+        eng.update_device(d_arena, nbytes, d_desc, n)
         k += 1
         if k % 16 == 0:
             eng.sync()
     eng.sync()
     t0 = time.perf_counter()
-    for k in range(steps):
-        a, b, d = batches[k % FRESH_BATCHES]
-        eng.update_device(a, b, d, n)
+    for _ in range(steps):
+        eng.update_device(d_arena, nbytes, d_desc, n)
     eng.sync()
     dt = (time.perf_counter() - t0) / steps
-    ev_ms = eng.time_update_batches(batches, n, steps) / steps
+    ev_ms = eng.time_update_device(d_arena, nbytes, d_desc, n, steps) / steps
     want = golden_digest(args.config, first, n)
-    digests = [f"{eng.digest_device(a, b, d, n, first):016x}" for a, b, d in batches]
-    for a, _, d, _ in extra:
-        a.free()
-        d.free()
-    return {"batches": FRESH_BATCHES, "steps": steps, "value": round(frame_bytes / dt / 1e9, 2),
-            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+    got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
+    return {"batches": 1, "steps": steps, "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
             "frac": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "frac_wall": round(algo_bytes / dt / 1e9 / HBM_PEAK_GBS, 4),
-            "timing": "frac: HIP events around the rotated calls on the engine's stream "
-                      "(nfcs_time_update_batches); value / frac_wall: wall clock",
-            "parity": None if want is None else all(g == want for g in digests)}
+            "timing": "frac: HIP events on the engine's stream; ms_per_step: wall clock",
+            "parity": None if want is None else got == want}
 
 
 def host_line(eng, args, n, reps: int = 3):

@@ -49,13 +49,16 @@ def test_two_ranks_one_gpu_bench_line():
     assert 0 < d["efficiency"] <= 1.1
 
 
-def test_one_gpu_line_carries_c4_shard_and_all_core_cpu_baseline():
-    """The N = 1 line (C1, BASELINE configs[1]) carries the C4-shard sub-line — the per-GPU batch the
-    N > 1 lines scale, with its own roofline fraction and the reference's digest of that shard — and
-    the CPU baseline on every CPU of the affinity set."""
+def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
+    """The N = 1 line (C1, BASELINE configs[1]) times the steady state — calls rotating over 4 separately
+    generated batches, every batch's digest the reference's — and carries the one-batch replay
+    sub-line, the C4-shard sub-line (the per-GPU batch the N > 1 lines scale, with its own roofline
+    fraction and the reference's digest of that shard), the host-memory (PCIe-inclusive) sub-line
+    from pinned and pageable arenas with the reference's digest, and the CPU baseline at the fastest
+    thread count measured."""
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8", "--warmup", "2", "--no-fresh",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8", "--warmup", "2",
            "--cpu-seconds", "1"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -63,11 +66,16 @@ def test_one_gpu_line_carries_c4_shard_and_all_core_cpu_baseline():
     assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["parity"]["match"] is True
+    assert d["roofline"]["batches_rotated"] == 4
+    assert d["replay"]["parity"] is True and 0.3 < d["replay"]["frac"] < 1.0
     c4 = d["c4_shard"]
-    assert c4["packets"] == 1 << 22 and c4["parity"]["match"] is True
+    assert c4["packets"] == 1 << 22 and c4["parity"]["match"] is True and c4["batches_rotated"] == 2
     assert 0.3 < c4["frac"] < 1.0 and c4["value"] > 0
+    h = d["host"]
+    assert h["parity"]["match"] is True and h["pinned"]["GBps"] > 0 and h["pageable"]["GBps"] > 0
     cb = d["cpu_baseline"]
-    assert cb["cores"] == cb["nproc"] == len(os.sched_getaffinity(0)) and cb["value"] > 0
+    assert cb["value"] == max(x["value"] for x in cb["runs"]) and cb["value"] > 0
+    assert max(x["threads"] for x in cb["runs"]) == cb["nproc"] == len(os.sched_getaffinity(0))
     sc = d["stream_ceiling"]
     assert sc["read_only_GBps"] == max(sc["forms_GBps"].values())
 

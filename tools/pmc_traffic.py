@@ -36,7 +36,7 @@ def run_pass(out, cfg, counters, steps, op="update", packets=0, align=128):
     d = os.path.join(out, f"c{cfg}{'_' + str(packets) if packets else ''}_a{align}_{op}_{counters[0]}")
     cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
-           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-fresh", "--no-c4", "--op", op, "--align", str(align)] + (["--packets", str(packets)] if packets else [])
+           "--steps", str(steps), "--warmup", "1", "--warm-seconds", "0", "--no-cpu", "--no-replay", "--no-host", "--no-c4", "--op", op, "--align", str(align)] + (["--packets", str(packets)] if packets else [])
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:

@@ -21,6 +21,11 @@
 //  30/31/32 every wave defers (SF_REC64, long shape): 64-byte header records + a write pass that
 //       stores each frame's first 64 bytes whole from them, past the caches / write-through / write-back
 //  33/34 the same in the short shape (C3's), past the caches / write-through
+//  40   the product's read pass + its write pass with the stores removed (timing only: the pass's
+//       loads, decisions and launch alone)
+//  41   the product's read pass + a write pass of 256 packets per wave (all four groups' descriptor
+//       and record loads issued first, then 16 store instructions); 42 the same kernel at 64 packets
+//       per wave (= the product's write pass, through this template)
 // Timing-only bounds (they write placeholder bytes: no parity):
 //  20   the read pass's loads alone (launch_frames_read: nothing computed or written)
 //  21   writes alone: 4 byte stores per packet at frame bytes 24, 25, 40, 41 (sc0 sc1 nt), no reads
@@ -152,6 +157,53 @@ __global__ __launch_bounds__(kBlock) void apply_rec64_kernel(uint8_t* __restrict
         st8_nt(f + a, (j < 2 ? (r.y >> (8 * j)) : (r.y >> (16 + 8 * (j - 2)))) & 0xFFu);
 }
 
+// apply_bytes_kernel with PW packets per wave (PW / 64 groups of 64, loads first) and, for NOSTORE,
+// every store removed (timing only)
+template <int G, bool NOSTORE>
+__global__ __launch_bounds__(kBlock) void apply_bytes_fat_kernel(uint8_t* __restrict__ arena,
+                                                                 const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                                 const nfcs_patch* __restrict__ rec) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    nfcs_desc d[G];
+    uint2 r0[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t i = (w * G + g) * 64u + lane;
+        d[g] = i < n ? desc[i] : nfcs_desc{0u, 0u};
+        r0[g] = i < n ? ((const uint2*)rec)[i] : make_uint2(0u, 0u);
+    }
+    const uint32_t j = lane & 3u;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t i = (w * G + g) * 64u + lane;
+        uint32_t s = defer_len(d[g].len);
+        s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xF, 0xF, true);
+        s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xF, 0xF, true);
+        const bool dfr = i < n && defer_group(s, 4);
+        const uint64_t mask = __builtin_amdgcn_ballot_w64(dfr);
+        if (!mask) continue;
+        const uint2 r = dfr ? r0[g] : make_uint2(NFCS_PATCH_NONE | (NFCS_PATCH_NONE << 16), 0u);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            if (((mask >> (16u * k)) & 0xFFFFu) == 0) continue;
+            const int q4 = (int)((16u * k + (lane >> 2)) * 4u);
+            const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.x);
+            const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)r.y);
+            const uint32_t o16 = (uint32_t)__builtin_amdgcn_ds_bpermute(q4, (int)d[g].off16);
+            const uint32_t ipo = rx & 0xFFFFu, l4o = rx >> 16;
+            const uint32_t off = j < 2 ? ipo : l4o;
+            const uint32_t a = off + (j & 1u);
+            const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
+            if (off != NFCS_PATCH_NONE && !overlap) {
+                const uint32_t b = (j < 2 ? (ry >> (8 * j)) : (ry >> (16 + 8 * (j - 2)))) & 0xFFu;
+                if (NOSTORE) asm volatile("" ::"v"(b), "v"(o16));
+                else st8_nt(arena + (uint64_t)o16 * 16u + a, b);
+            }
+        }
+    }
+}
+
 static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_desc* desc, uint32_t n,
                             nfcs_patch* ws, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0, nullptr};
@@ -189,6 +241,11 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
     case 32: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<0>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
     case 33: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
     case 34: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 40: ROWS(SF_DEFER); hipLaunchKernelGGL((apply_bytes_fat_kernel<1, true>), dim3(gb), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 41: ROWS(SF_DEFER);
+        hipLaunchKernelGGL((apply_bytes_fat_kernel<4, false>), dim3((n + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), 0, st, arena, desc, n, ws);
+        break;
+    case 42: ROWS(SF_DEFER); hipLaunchKernelGGL((apply_bytes_fat_kernel<1, false>), dim3(gb), dim3(kBlock), 0, st, arena, desc, n, ws); break;
     case 20: {
         static unsigned long long* sink = nullptr;
         if (!sink && hipMalloc(&sink, 64) != hipSuccess) return hipErrorOutOfMemory;
