@@ -723,8 +723,12 @@ DEV uint4 hdr_view(const RowStage<K>& S, uint32_t rowbase4, uint32_t rl) {
     return a < (uint32_t)R ? r0 : r1;
 }
 
-template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false, int SEC = 0>
-DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
+// COLD = false: rows with an uncommon header are left alone (nothing stored for them) and the call
+// returns true when the wave has any, for the caller to run them later with COLD = true.
+// KC: slots per continuation batch of frames longer than R*K chunks (fewer: fewer live registers).
+template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false, int SEC = 0,
+          bool COLD = true, int KC = K>
+DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
                      const uint32_t* wmac = nullptr, const nfcs_nexthop* table = nullptr) {
     const uint32_t len = S.len;
@@ -839,15 +843,15 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     }
     // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t cmax = wave_max_rows<R>(LA ? nre + S.mis : nre);
-    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
-        uint4 w[K];
+    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * KC) {
+        uint4 w[KC];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
+        for (int k = 0; k < KC; ++k) {
             const uint32_t c = cb + rlv + (uint32_t)R * k - S.mis;
             w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
+        for (int k = 0; k < KC; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
     }
     const uint32_t z = row_sum<R>(acc) + P.corr;
     if (P.flags & F_L4) {
@@ -928,6 +932,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
+    if (!COLD) return __builtin_amdgcn_ballot_w64(slow) != 0;
     if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
         // Uncommon headers, handled last so that only the frame address and length are live
         // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
@@ -1000,6 +1005,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         // the forward stored everything of an uncommon header here: nothing left for the write pass
         if (FWD && DFR && rec && slow && rl == 0) ((uint2*)rec)[S.p] = make_uint2(0xFFFFFFFFu, 0u);
     }
+    return false;
 }
 
 // One wave = 64/R packet rows; one workgroup per BS/R packets, as many workgroups as the batch

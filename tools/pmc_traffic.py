@@ -27,7 +27,7 @@ PACKETS = {0: 1024, 1: 1 << 20, 2: 1 << 20, 3: 1 << 22}
 # the kernels of one call of the op: nfcs_update_device is the read pass and, for waves of long
 # frames, the write pass (apply_bytes_kernel); per call = the sum of the per-kernel medians
 KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("update_rows_kernel", "apply_fwd_kernel"),
-          "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_kernel",)}
+          "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_lanes_kernel",)}
 
 
 def run_pass(out, cfg, counters, steps, op="update", packets=0, align=128):

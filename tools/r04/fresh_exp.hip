@@ -17,6 +17,8 @@
 //  11/12/13 the short shape (16-lane rows, one-wave workgroups at 7 waves/SIMD, C3's) storing each
 //       frame's first 64 bytes whole past the caches / write-through / write-back
 //  14   the short shape with its inline byte stores (the product's form for C3)
+//  16-19 the short shape (inline stores) with other slot counts / occupancy caps: K 6 at 8 waves/SIMD,
+//       K 5 at 7 and 8, K 4 at 8 (longer frames continue in further row passes)
 //  15   the short shape writing patch records only (C3's read floor in its own shape; no parity)
 //  30/31/32 every wave defers (SF_REC64, long shape): 64-byte header records + a write pass that
 //       stores each frame's first 64 bytes whole from them, past the caches / write-through / write-back
@@ -26,6 +28,10 @@
 //  41   the product's read pass + a write pass of 256 packets per wave (all four groups' descriptor
 //       and record loads issued first, then 16 store instructions); 42 the same kernel at 64 packets
 //       per wave (= the product's write pass, through this template)
+//  50-55 the short shape software-pipelined: one wave walks G groups of 4 packets, issuing group
+//       g+1's chunk loads before processing group g (two RowStage buffers): G = 2 / 4 / 8 at
+//       6 waves/SIMD (50/51/52), G = 4 / 8 / 16 at 5 (53/54/55); the fast path inside the pipeline,
+//       groups with an uncommon header re-run alone at the end (row_process<..., COLD = false>)
 // Timing-only bounds (they write placeholder bytes: no parity):
 //  20   the read pass's loads alone (launch_frames_read: nothing computed or written)
 //  21   writes alone: 4 byte stores per packet at frame bytes 24, 25, 40, 41 (sc0 sc1 nt), no reads
@@ -204,6 +210,68 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_fat_kernel(uint8_t* __rest
     }
 }
 
+// The short shape, software-pipelined (variants 50-55): a one-wave workgroup walks G groups of PW
+// packets; group g+1's descriptors and chunk loads are in flight while group g is processed and
+// stored, so the wave's memory pipe never idles behind its own arithmetic.
+template <int K, int R, int G, int OCC, int KCP = 1>
+__global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                            uint32_t nblocks, uint8_t* __restrict__ arena,
+                                                            uint64_t arena_bytes, uint32_t base16,
+                                                            uint8_t* __restrict__ status) {
+    static_assert(G <= 64, "one bit per group");
+    constexpr uint32_t PW = 64 / R;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t p0 = (uint64_t)xcd_block_n(nblocks) * (G * PW);
+    if (p0 >= n) return;
+    // the fast path only inside the pipeline (the cold path's calls would keep the other stage's
+    // registers live across them); groups with an uncommon header are re-run at the end, alone
+    uint64_t cold = 0;
+    {
+        RowStage<K> A, B;
+        DescW<PW> DA = load_descw<PW>(desc, p0, n);
+        DescW<PW> DB = load_descw<PW>(desc, p0 + PW, n);
+        row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), p0 + row, n, base16, rl);
+#pragma unroll 1
+        for (int g = 0; g < G; g += 2) {
+            const uint64_t pa = p0 + (uint64_t)g * PW, pb = pa + PW;
+            if (pb >= n) {  // wave-uniform: the last group of the batch
+                if (row_process<K, R, false, true, false, false, 0, false, KCP>(A, rl, rowbase4, status, nullptr, true))
+                    cold |= 1ull << g;
+                break;
+            }
+            if (g + 2 < G) DA = load_descw<PW>(desc, pa + 2 * PW, n);
+            row_stage<K, R, false, false>(B, arena, arena_bytes, pick_desc<PW>(DB, row), pb + row, n, base16, rl);
+            if (row_process<K, R, false, true, false, false, 0, false, KCP>(A, rl, rowbase4, status, nullptr, true))
+                cold |= 1ull << g;
+            const uint64_t pc = pb + PW;
+            if (g + 2 < G && pc < n) {
+                if (g + 3 < G) DB = load_descw<PW>(desc, pc + PW, n);
+                row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), pc + row, n, base16, rl);
+            }
+            if (row_process<K, R, false, true, false, false, 0, false, KCP>(B, rl, rowbase4, status, nullptr, true))
+                cold |= 1ull << (g + 1);
+            if (pc >= n) break;
+        }
+    }
+    while (cold) {  // wave-uniform; rare (IP options, IHL < 5, headers past the frame)
+        const int g = __builtin_ctzll(cold);
+        cold &= cold - 1;
+        const uint64_t pg = p0 + (uint64_t)g * PW;
+        RowStage<K> C;
+        row_stage<K, R, false, false>(C, arena, arena_bytes, pick_desc<PW>(load_descw<PW>(desc, pg, n), row), pg + row,
+                                      n, base16, rl);
+        row_process<K, R, false, true, false, false, 0, true>(C, rl, rowbase4, status, nullptr, true);
+    }
+}
+
+template <int G, int OCC>
+static void launch_pipe(uint8_t* arena, uint64_t bytes, const nfcs_desc* desc, uint32_t n, hipStream_t st) {
+    const uint32_t grid = (uint32_t)(((uint64_t)n + 4 * G - 1) / (4 * G));
+    hipLaunchKernelGGL((update_pipe_kernel<6, 16, G, OCC>), dim3(grid), dim3(64), 0, st, desc, n, grid, arena, bytes,
+                       0u, (uint8_t*)nullptr);
+}
+
 static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_desc* desc, uint32_t n,
                             nfcs_patch* ws, hipStream_t st) {
     const FwdArgs nofwd = {nullptr, nullptr, 0, nullptr};
@@ -234,6 +302,10 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
     case 12: SHORT(SF_SECTOR_WT); break;
     case 13: SHORT(SF_SECTOR_WB); break;
     case 14: SHORT(SF_INLINE); break;
+    case 16: launch_rows<6, 16, 8, 64, false, SF_INLINE, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
+    case 17: launch_rows<5, 16, 7, 64, false, SF_INLINE, 0, 5>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
+    case 18: launch_rows<5, 16, 8, 64, false, SF_INLINE, 0, 5>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
+    case 19: launch_rows<4, 16, 8, 64, false, SF_INLINE, 0, 4>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
     case 15: launch_rows<6, 16, 7, 64, false, SF_RECORDS, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr,
                                                               ws, ws, nofwd); break;
     case 30: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
@@ -246,6 +318,14 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
         hipLaunchKernelGGL((apply_bytes_fat_kernel<4, false>), dim3((n + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), 0, st, arena, desc, n, ws);
         break;
     case 42: ROWS(SF_DEFER); hipLaunchKernelGGL((apply_bytes_fat_kernel<1, false>), dim3(gb), dim3(kBlock), 0, st, arena, desc, n, ws); break;
+    case 50: launch_pipe<2, 6>(arena, bytes, desc, n, st); break;
+    case 51: launch_pipe<4, 6>(arena, bytes, desc, n, st); break;
+    case 52: launch_pipe<8, 6>(arena, bytes, desc, n, st); break;
+    case 53: launch_pipe<4, 5>(arena, bytes, desc, n, st); break;
+    case 54: launch_pipe<8, 5>(arena, bytes, desc, n, st); break;
+    case 55: launch_pipe<16, 5>(arena, bytes, desc, n, st); break;
+    case 56: launch_pipe<4, 4>(arena, bytes, desc, n, st); break;
+    case 57: launch_pipe<8, 4>(arena, bytes, desc, n, st); break;
     case 20: {
         static unsigned long long* sink = nullptr;
         if (!sink && hipMalloc(&sink, 64) != hipSuccess) return hipErrorOutOfMemory;
