@@ -470,8 +470,23 @@ def main():
     l3 = args.op == "l3fwd"
     fk = args.op == "flowkey"
     extra_roofline = {}
+    # The steady state of a NIC ring, for every op: the calls rotate over `nrot`
+    # separately generated batches, so no call re-processes what the previous call wrote and no
+    # header line is still in the memory-side cache from an earlier pass over the same frames.
+    # 4 batches up to 1M packets (4 x 128 MB of header lines > the 256 MB Infinity Cache), 2 above
+    # (a 4M batch alone is 25x the cache). --batches 1 replays one batch.
+    nrot = args.batches or (FRESH_BATCHES if n <= (1 << 20) else 2)
+    batches = [(d_arena, nbytes, d_desc)] + [eng.config_batch(args.config, SEED, first, n, args.align)[:3]
+                                             for _ in range(nrot - 1)]
+    ctr = [0]
+
+    def nxt():
+        k = ctr[0]
+        ctr[0] += 1
+        return k, batches[k % nrot]
     if l3:
-        # every launch decrements TTL (64 in the generator): K + 1 launches per fresh batch
+        # every launch decrements TTL (64 in the generator): each batch is forwarded once per nrot
+        # timed steps, and every batch is regenerated before the timed steps
         if args.steps > 60:
             raise SystemExit("--op l3fwd: --steps <= 60 (TTL 64 runs out after 63 forwards)")
         g3 = golden()["l3fwd_c1"]
@@ -479,9 +494,16 @@ def main():
         d_tab = eng.alloc(table.nbytes).upload(table)
         d_nh = eng.alloc(4 * n).upload(((np.arange(first, first + n)) % 9).astype(np.uint32))
         algo_bytes = frame_bytes + 37.0 * n  # + 4 csum + 12 MAC + 1 TTL written, 8 desc + 4 nh + 8 table read
-        step = lambda: eng.l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8)
-        regen = lambda: (eng.gen_config_device(args.config, SEED, first, n, d_arena, nbytes, d_desc),
-                         eng.sync())
+
+        def step():
+            _, (a, b, d) = nxt()
+            eng.l3_forward_device(a, b, d, d_nh, n, d_tab, 8)
+
+        def regen():
+            for a, b, d in batches:
+                eng.gen_config_device(args.config, SEED, first, n, a, b, d)
+            eng.sync()
+            ctr[0] = 0
     elif fk:
         d_keys = eng.alloc(64 * n)
         d_hash = eng.alloc(4 * n)
@@ -492,37 +514,32 @@ def main():
         hdr = float(np.minimum(hdesc["len"].astype(np.float64), 128.0).sum())
         algo_bytes = hdr + 76.0 * n
         needed = float(np.minimum(hdesc["len"].astype(np.float64), 82.0).sum()) + 76.0 * n
-        step = lambda: eng.flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash)
+
+        def step():
+            _, (a, b, d) = nxt()
+            eng.flow_keys_device(a, b, d, n, d_keys, d_hash)
         regen = lambda: None
     elif args.op == "vlan":
         if args.config != 1:
             raise SystemExit("--op vlan: config 1 (1536-byte buffers per 1500-byte frame)")
-        # push_vlan(100, 3) and pop_vlan() alternate, each on every frame; per packet the pass
-        # reads the frame, writes it back from byte 12 (moved by 4 bytes) and updates its length:
-        # push 2*len + 4 B, pop (len' = len + 4) 2*len' - 4 B; +8 B descriptor read, 4 B written
+        # push_vlan(100, 3) and pop_vlan() alternate on each batch (round r of the rotation pushes
+        # when r is even, pops when odd), each on every frame; per packet the pass reads the frame,
+        # writes it back from byte 12 (moved by 4 bytes) and updates its length: push 2*len + 4 B,
+        # pop (len' = len + 4) 2*len' - 4 B; +8 B descriptor read, 4 B written
         VPUSH, VCAP = nf.vlan_push_op(100, 3), 1536
-        flip = [0]
 
         def step():
-            eng.vlan_device(d_arena, nbytes, d_desc, n, None, VPUSH if flip[0] == 0 else nf.VLAN_POP,
-                            None, VCAP)
-            flip[0] ^= 1
+            k, (a, b, d) = nxt()
+            eng.vlan_device(a, b, d, n, None, VPUSH if (k // nrot) % 2 == 0 else nf.VLAN_POP, None, VCAP)
         algo_bytes = 2.0 * frame_bytes + 4.0 * n + 12.0 * n
-        regen = lambda: step() if flip[0] else None  # back to untagged frames (pop)
-    else:
-        # The steady state of a NIC ring: the calls rotate over `nrot`
-        # separately generated batches, so no call re-processes what the previous call wrote and
-        # no header line is still in the memory-side cache from an earlier pass over the same
-        # frames. 4 batches up to 1M packets (4 x 128 MB of header lines > the 256 MB Infinity
-        # Cache), 2 above (a 4M batch alone is 25x the cache). --batches 1 replays one batch.
-        nrot = args.batches or (FRESH_BATCHES if n <= (1 << 20) else 2)
-        extra = [eng.config_batch(args.config, SEED, first, n, args.align)[:3] for _ in range(nrot - 1)]
-        batches = [(d_arena, nbytes, d_desc)] + extra
-        ctr = [0]
 
+        def regen():  # back to untagged frames: complete the round of pops
+            while ctr[0] % (2 * nrot):
+                step()
+            eng.sync()
+    else:
         def step():
-            a, b, d = batches[ctr[0] % nrot]
-            ctr[0] += 1
+            _, (a, b, d) = nxt()
             eng.update_device(a, b, d, n)
         regen = lambda: None
 
@@ -559,8 +576,7 @@ def main():
     got = None
     if l3:
         regen()
-        ev_ms = eng.time_l3_forward_device(d_arena, nbytes, d_desc, d_nh, n, d_tab, 8,
-                                           args.steps) / args.steps
+        ev_ms = event_ms(eng, step, args.steps) / args.steps
         # parity: one forward of a fresh batch vs the reference's digest (C1, rank 0 shard)
         regen()
         step()
@@ -571,22 +587,21 @@ def main():
                 want = g["digest_out"]
     elif args.op == "vlan":
         regen()
-        ev_ms = eng.time_vlan_device(d_arena, nbytes, d_desc, n, VPUSH, nf.VLAN_POP, VCAP,
-                                     2 * ((args.steps + 1) // 2)) / (2 * ((args.steps + 1) // 2))
+        vsteps = 2 * nrot * -(-args.steps // (2 * nrot))  # whole push + pop rounds: ends untagged
+        ev_ms = event_ms(eng, step, vsteps) / vsteps
         # parity: one push of the untagged batch vs the reference's digest, then one pop
         gv = golden().get("vlan_c1", {})
         on_ref = first == 0 and n == gv.get("n")
-        step()
+        eng.vlan_device(d_arena, nbytes, d_desc, n, None, VPUSH, None, VCAP)
         eng.sync()
         got_push = f"{eng.digest_device(d_arena, nbytes, d_desc, n, first):016x}"
-        step()
+        eng.vlan_device(d_arena, nbytes, d_desc, n, None, nf.VLAN_POP, None, VCAP)
         eng.sync()
         want = gv.get("digest_push_pop") if on_ref else golden_digest(1, first, n)
         if on_ref and got_push != gv["digest_push"]:
             want = "push digest " + gv["digest_push"] + " != " + got_push
     elif fk:
-        ev_ms = eng.time_flow_keys_device(d_arena, nbytes, d_desc, n, d_keys, d_hash,
-                                          args.steps) / args.steps
+        ev_ms = event_ms(eng, step, args.steps) / args.steps
         # parity: digest of the 64-byte records (they hold the hashes too) vs the reference's; the
         # records depend on the frames' bytes only, so the digest holds at any --align
         gk = golden().get("flowkey_c1", {})
@@ -605,6 +620,10 @@ def main():
                           "needed_bytes_per_packet": "min(len, 82) header + 8 descriptor + 64 record + 4 hash",
                           "frac_is_on": "min(len, 128): the frame's first 128-byte line, the two 64-byte "
                                         "sectors the 82 header bytes span"}
+    if args.op != "update":
+        extra_roofline["batches_rotated"] = nrot
+        extra_roofline["kernel_ms_timing"] = ("HIP events (torch.cuda.Event on the engine's own stream, "
+                                              "torch.cuda.ExternalStream) around the rotated calls")
     else:
         # the same rotation, HIP events on the engine's stream around all the calls
         ev_ms = eng.time_update_batches(batches, n, args.steps) / args.steps
@@ -636,10 +655,10 @@ def main():
     parity["all_ranks"] = D.sum(0.0 if parity_ok is False else 1.0) == ws
 
     replay = None
+    for a, _, d in batches[1:]:
+        a.free()
+        d.free()
     if args.op == "update":
-        for a, _, d in batches[1:]:
-            a.free()
-            d.free()
         if ws == 1 and not args.no_replay and nrot > 1:
             replay = replay_line(eng, args, first, n, algo_bytes, d_arena, nbytes, d_desc)
 
@@ -766,6 +785,20 @@ def scaling_timings(D, timed, frame_bytes: float, steps: int, solo_first: bool, 
     t_rank = timed()
     D.barrier()
     return solo, t_rank, D.max(t_rank)
+
+
+def event_ms(eng, step, steps: int) -> float:
+    """Milliseconds between two HIP events recorded on the engine's own stream (wrapped as a torch
+    ExternalStream) around `steps` step() calls, which launch on that stream."""
+    import torch
+    st = torch.cuda.ExternalStream(eng.stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        step()
+    e1.record(st)
+    e1.synchronize()
+    return float(e0.elapsed_time(e1))
 
 
 def timed_steps(eng, step, steps: int, regen=None) -> float:
