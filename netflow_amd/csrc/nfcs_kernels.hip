@@ -675,17 +675,11 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 //               evicted from the memory-side cache into, the read stream); other waves as SF_INLINE;
 //   SF_RECORDS  patch records only, frames untouched (nfcs_update_host: only the records cross
 //               PCIe back).
-//   SF_SECTOR_* (round 4, measured) like SF_INLINE, but lanes 0-3 of the row store the frame's first
-//               64 bytes whole with the 2+2 bytes patched in (one full 64-byte write, no partial
-//               line), past the caches / write-through / write-back; rows whose fields lie past
-//               byte 63 or whose frame is shorter than 64 bytes store bytes as SF_INLINE.
-//   SF_REC64    (round 4, measured) every wave defers: rows whose fields lie below byte 63 write their
-//               patched first 64 bytes as a dense 64-byte record (at kRec64Records records past the
-//               8-byte records) and the 8-byte record kRec64Flag; the write pass stores them whole.
-enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2, SF_SECTOR_NT = 3, SF_SECTOR_WT = 4, SF_SECTOR_WB = 5,
-             SF_REC64 = 6 };
-constexpr uint32_t kRec64Records = 1u << 22;
-constexpr uint32_t kRec64Flag = 0xFFFEFFFEu;
+// Round 4 measured, under rotating batches, forms storing each frame's first 64 bytes whole (from
+// the read pass, or from 64-byte records through a write pass) and write passes of write-back /
+// write-through stores: all slower than SF_DEFER's masked `nt` stores (their code is
+// in git 2288ac5, tools/r04/fresh_exp.hip variants 4-8, 11-13, 30-34).
+enum : int { SF_INLINE = 0, SF_DEFER = 1, SF_RECORDS = 2 };
 // The fused forward's deferred record (large bursts, SF_DEFER; the write pass apply_fwd_kernel is
 // its only reader), 8 bytes for a forwarded frame with a common header, all offsets below 64:
 //   x = ip_off | ttl' << 8 | proto << 16 | l4_off << 24, y = ip checksum bytes | l4 checksum bytes << 16
@@ -726,7 +720,7 @@ DEV uint4 hdr_view(const RowStage<K>& S, uint32_t rowbase4, uint32_t rl) {
 // COLD = false: rows with an uncommon header are left alone (nothing stored for them) and the call
 // returns true when the wave has any, for the caller to run them later with COLD = true.
 // KC: slots per continuation batch of frames longer than R*K chunks (fewer: fewer live registers).
-template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false, int SEC = 0,
+template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false,
           bool COLD = true, int KC = K>
 DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
@@ -906,29 +900,6 @@ DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         emit(S.valid && !slow, st, ipw, l4w, false, !DFR);
         if (DFR && rec && S.valid && !slow && rl == 0)
             ((uint2*)rec)[S.p] = (fwd && live) ? fwd_record(ipw, l4w, ttl - 1u, proto, tagged) : make_uint2(0xFFFFFFFFu, 0u);
-    } else if (SEC == 4) {
-        // SF_REC64: the patched first 64 bytes as a dense record, the 8-byte record flagged
-        const uint32_t ipo = ipw & 0xFFFFu, l4o = l4w & 0xFFFFu;
-        const bool sec = S.valid && !slow && len >= 64u &&
-                         (ipo == NFCS_PATCH_NONE || ipo < 63u) && (l4o == NFCS_PATCH_NONE || l4o < 63u) &&
-                         (ipo != NFCS_PATCH_NONE || l4o != NFCS_PATCH_NONE);
-        if (sec && rl < 4 && rec)
-            ((uint4*)(rec + kRec64Records))[(uint64_t)S.p * 4u + rl] = put_field(put_field(h0, ipw, rl), l4w, rl);
-        emit(S.valid && !slow, st, sec ? 0xFFFEu : ipw, sec ? 0xFFFEu : l4w, false);
-    } else if (SEC) {
-        // the frame's first 64 bytes whole (SF_SECTOR_*): lanes 0-3 store frame chunks 0-3 with the
-        // fields patched in, when both fields lie below byte 63 and the frame has 64 bytes
-        const uint32_t ipo = ipw & 0xFFFFu, l4o = l4w & 0xFFFFu;
-        const bool sec = S.valid && !slow && frame_stores && len >= 64u &&
-                         (ipo == NFCS_PATCH_NONE || ipo < 63u) && (l4o == NFCS_PATCH_NONE || l4o < 63u) &&
-                         (ipo != NFCS_PATCH_NONE || l4o != NFCS_PATCH_NONE);
-        if (sec && rl < 4) {
-            const uint4 v = put_field(put_field(h0, ipw, rl), l4w, rl);
-            if (SEC == 1) st16_nt((uint4*)frame + rl, v);
-            else if (SEC == 2) st16<true>((uint4*)frame + rl, v);
-            else st16<false>((uint4*)frame + rl, v);
-        }
-        emit(S.valid && !slow, st, ipw, l4w, frame_stores && !sec);
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
@@ -1026,8 +997,8 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
                    uint32_t rl, uint32_t row, uint32_t rowbase4, bool defer, const uint32_t (&q)[PW],
                    uint8_t* status, nfcs_patch* patch, nfcs_patch* ws, const nfcs_nexthop* table, uint32_t table_n) {
     typedef const __attribute__((address_space(4))) uint32_t cu32;
-    const bool frame_stores = SF == SF_INLINE || (SF >= SF_SECTOR_NT && SF <= SF_SECTOR_WB) || (SF == SF_DEFER && !defer);
-    nfcs_patch* rec = patch ? patch : ((defer || SF == SF_REC64) ? ws : nullptr);
+    const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
+    nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
     RowStage<K> S;
     row_stage<K, R, FWD, LA>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
@@ -1048,7 +1019,7 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     }
     // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
     // workgroups), write-through elsewhere (see row_process)
-    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER, LA, (SF >= SF_SECTOR_NT && SF <= SF_SECTOR_WB) ? SF - 2 : (SF == SF_REC64 ? 4 : 0)>(S, rl, rowbase4, status, rec,
+    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER, LA>(S, rl, rowbase4, status, rec,
                                                                                  frame_stores, table_n, wmac, table);
 }
 

@@ -8,21 +8,21 @@
 //   0   the product (launch_update, kUpdateAuto)
 //   1   read pass writing patch records only, frames untouched (the floor: no frame writes)
 //   2/3 the product's read pass + its write pass with write-back / write-through (sc1) byte stores
-//   4/5/6 read pass storing each frame's first 64 bytes whole, past the caches / write-through /
-//       write-back (SF_SECTOR_*), no write pass
+//   4/5/6 (git 2288ac5) read pass storing each frame's first 64 bytes whole, past the caches /
+//       write-through / write-back (SF_SECTOR_*, since removed from the product), no write pass
 //   7/8 the product's read pass + a write pass that re-reads each deferred frame's first 64 bytes and
 //       stores them whole with the bytes patched in, past the caches / write-through
 //   9   every wave inline (SF_INLINE: byte stores, sc1), no write pass
 //  10   the product in 512K-packet sub-batches (its form above 1M packets) at any n
-//  11/12/13 the short shape (16-lane rows, one-wave workgroups at 7 waves/SIMD, C3's) storing each
-//       frame's first 64 bytes whole past the caches / write-through / write-back
+//  11/12/13 (git 2288ac5) the short shape (16-lane rows, one-wave workgroups at 7 waves/SIMD, C3's)
+//       storing each frame's first 64 bytes whole past the caches / write-through / write-back
 //  14   the short shape with its inline byte stores (the product's form for C3)
 //  16-19 the short shape (inline stores) with other slot counts / occupancy caps: K 6 at 8 waves/SIMD,
 //       K 5 at 7 and 8, K 4 at 8 (longer frames continue in further row passes)
 //  15   the short shape writing patch records only (C3's read floor in its own shape; no parity)
-//  30/31/32 every wave defers (SF_REC64, long shape): 64-byte header records + a write pass that
-//       stores each frame's first 64 bytes whole from them, past the caches / write-through / write-back
-//  33/34 the same in the short shape (C3's), past the caches / write-through
+//  30/31/32 (git 2288ac5) every wave defers (SF_REC64, long shape): 64-byte header records + a write
+//       pass storing each frame's first 64 bytes whole from them, past the caches / write-through /
+//       write-back; 33/34 the same in the short shape (C3's)
 //  40   the product's read pass + its write pass with the stores removed (timing only: the pass's
 //       loads, decisions and launch alone)
 //  41   the product's read pass + a write pass of 256 packets per wave (all four groups' descriptor
@@ -136,33 +136,6 @@ __global__ __launch_bounds__(kBlock) void write_only_kernel(uint8_t* __restrict_
     else st16<true>((uint4*)f + j, make_uint4(j, 1u, 2u, 3u));
 }
 
-// SF_REC64's write pass: 4 lanes per packet; a flagged packet's 64-byte record (dense, coalesced)
-// goes into its frame's first 64 bytes whole, other records as byte stores.
-template <int POL>  // 0 write-back, 1 write-through (sc1), 2 past the caches
-__global__ __launch_bounds__(kBlock) void apply_rec64_kernel(uint8_t* __restrict__ arena,
-                                                             const nfcs_desc* __restrict__ desc, uint32_t n,
-                                                             const nfcs_patch* __restrict__ rec) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t p = t >> 2;
-    const uint32_t j = (uint32_t)t & 3u;
-    if (p >= n) return;
-    const nfcs_desc d = desc[p];
-    const uint2 r = ((const uint2*)rec)[p];
-    uint8_t* f = arena + (uint64_t)d.off16 * 16u;
-    if (r.x == kRec64Flag) {
-        const uint4 v = ((const uint4*)(rec + kRec64Records))[p * 4u + j];
-        if (POL == 2) st16_nt((uint4*)f + j, v);
-        else st16<POL == 1>((uint4*)f + j, v);
-        return;
-    }
-    const uint32_t ipo = r.x & 0xFFFFu, l4o = r.x >> 16;
-    const uint32_t off = j < 2 ? ipo : l4o;
-    const uint32_t a = off + (j & 1u);
-    const bool overlap = j < 2 && l4o != NFCS_PATCH_NONE && (a == l4o || a == l4o + 1u);
-    if (off != NFCS_PATCH_NONE && !overlap)
-        st8_nt(f + a, (j < 2 ? (r.y >> (8 * j)) : (r.y >> (16 + 8 * (j - 2)))) & 0xFFu);
-}
-
 // apply_bytes_kernel with PW packets per wave (PW / 64 groups of 64, loads first) and, for NOSTORE,
 // every store removed (timing only)
 template <int G, bool NOSTORE>
@@ -236,20 +209,20 @@ __global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* _
         for (int g = 0; g < G; g += 2) {
             const uint64_t pa = p0 + (uint64_t)g * PW, pb = pa + PW;
             if (pb >= n) {  // wave-uniform: the last group of the batch
-                if (row_process<K, R, false, true, false, false, 0, false, KCP>(A, rl, rowbase4, status, nullptr, true))
+                if (row_process<K, R, false, true, false, false, false, KCP>(A, rl, rowbase4, status, nullptr, true))
                     cold |= 1ull << g;
                 break;
             }
             if (g + 2 < G) DA = load_descw<PW>(desc, pa + 2 * PW, n);
             row_stage<K, R, false, false>(B, arena, arena_bytes, pick_desc<PW>(DB, row), pb + row, n, base16, rl);
-            if (row_process<K, R, false, true, false, false, 0, false, KCP>(A, rl, rowbase4, status, nullptr, true))
+            if (row_process<K, R, false, true, false, false, false, KCP>(A, rl, rowbase4, status, nullptr, true))
                 cold |= 1ull << g;
             const uint64_t pc = pb + PW;
             if (g + 2 < G && pc < n) {
                 if (g + 3 < G) DB = load_descw<PW>(desc, pc + PW, n);
                 row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), pc + row, n, base16, rl);
             }
-            if (row_process<K, R, false, true, false, false, 0, false, KCP>(B, rl, rowbase4, status, nullptr, true))
+            if (row_process<K, R, false, true, false, false, false, KCP>(B, rl, rowbase4, status, nullptr, true))
                 cold |= 1ull << (g + 1);
             if (pc >= n) break;
         }
@@ -261,7 +234,7 @@ __global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* _
         RowStage<K> C;
         row_stage<K, R, false, false>(C, arena, arena_bytes, pick_desc<PW>(load_descw<PW>(desc, pg, n), row), pg + row,
                                       n, base16, rl);
-        row_process<K, R, false, true, false, false, 0, true>(C, rl, rowbase4, status, nullptr, true);
+        row_process<K, R, false, true, false, false, true>(C, rl, rowbase4, status, nullptr, true);
     }
 }
 
@@ -285,9 +258,6 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
     case 1: ROWS(SF_RECORDS); break;
     case 2: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_bytes_pol_kernel<0>, dim3(gb), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
     case 3: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_bytes_pol_kernel<1>, dim3(gb), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
-    case 4: ROWS(SF_SECTOR_NT); break;
-    case 5: ROWS(SF_SECTOR_WT); break;
-    case 6: ROWS(SF_SECTOR_WB); break;
     case 7: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_sector_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
     case 8: ROWS(SF_DEFER); hipLaunchKernelGGL(apply_sector_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, 0u, ws); break;
     case 9: ROWS(SF_INLINE); break;
@@ -298,9 +268,6 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
             if (e != hipSuccess) return e;
         }
         break;
-    case 11: SHORT(SF_SECTOR_NT); break;
-    case 12: SHORT(SF_SECTOR_WT); break;
-    case 13: SHORT(SF_SECTOR_WB); break;
     case 14: SHORT(SF_INLINE); break;
     case 16: launch_rows<6, 16, 8, 64, false, SF_INLINE, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
     case 17: launch_rows<5, 16, 7, 64, false, SF_INLINE, 0, 5>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
@@ -308,11 +275,6 @@ static hipError_t r4_launch(int v, uint8_t* arena, uint64_t bytes, const nfcs_de
     case 19: launch_rows<4, 16, 8, 64, false, SF_INLINE, 0, 4>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr, nullptr, ws, nofwd); break;
     case 15: launch_rows<6, 16, 7, 64, false, SF_RECORDS, 0, 6>((n + 3u) / 4u, 0u, st, arena, bytes, desc, n, 0u, nullptr,
                                                               ws, ws, nofwd); break;
-    case 30: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
-    case 31: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
-    case 32: ROWS(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<0>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
-    case 33: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<2>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
-    case 34: SHORT(SF_REC64); hipLaunchKernelGGL(apply_rec64_kernel<1>, dim3(gs), dim3(kBlock), 0, st, arena, desc, n, ws); break;
     case 40: ROWS(SF_DEFER); hipLaunchKernelGGL((apply_bytes_fat_kernel<1, true>), dim3(gb), dim3(kBlock), 0, st, arena, desc, n, ws); break;
     case 41: ROWS(SF_DEFER);
         hipLaunchKernelGGL((apply_bytes_fat_kernel<4, false>), dim3((n + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), 0, st, arena, desc, n, ws);
