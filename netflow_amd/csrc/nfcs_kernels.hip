@@ -350,6 +350,47 @@ DEV RPlan fast_l4(const RowHdr<R>& V, RPlan P, uint32_t lenv, uint32_t v4, uint3
     return P;
 }
 
+// fast_l4 for IPv4 with IHL 5 (l4 = 34 in view coordinates), its three protocol branches evaluated
+// side by side and merged by selects: every field sits at a compile-time offset (one row_newbcast per
+// dword), so a wave whose rows carry different protocols (C3 mixes TCP and UDP in most waves) runs one
+// pass instead of one per protocol, and the checksum field's bytes are read at their constant offsets
+// instead of through two runtime-indexed ds_bpermute round trips. Same conditions and values as
+// fast_l4 (packet.hpp:773-889).
+template <int R>
+DEV RPlan fast_l4_v4(const RowHdr<R>& V, RPlan P, uint32_t lenv, uint32_t proto, uint32_t sh) {
+    const bool isT = proto == 6, isU = proto == 17, isI = proto == 1;
+    const uint32_t d4 = V.dw(4), d6 = V.dw(6), d7 = V.dw(7), d8 = V.dw(8);
+    const uint32_t d9 = V.dw(9), d10 = V.dw(10), d11 = V.dw(11), d12 = V.dw(12);
+    const uint32_t tl = bswap16(d4 & 0xFFFFu);  // total length (bytes 16-17)
+    const uint32_t lu = bswap16(d9 >> 16);      // udp.length (bytes 38-39)
+    const uint32_t hl = (d11 >> 18) & 0x3Cu;    // TCP data offset * 4 (byte 46, high nibble)
+    const uint32_t L = isU ? lu : ((tl - 20u) & 0xFFFFu);
+    // the conditions combined with non-short-circuit & so they stay selects, not branches
+    const bool inl = (34u + L <= lenv) & (42u <= lenv);
+    const bool ok = (isT & (53u <= lenv) & (tl >= 20u) & (L >= hl) & inl) |  // sizeof(TcpHeader) == 19
+                    (isU & (lu >= 8u) & inl) | (isI & (tl >= 20u) & (L >= 8u) & inl);
+    const uint32_t fs = isT ? 49u : (isU ? 40u : 36u), re = 34u + L;
+    // the raw field bytes the reference zeroes (LE weights): TCP 49 (high byte of word 48) and 50
+    // (low byte of word 50), each only inside the region; UDP 40-41, ICMP 36-37 (always inside: L >= 8)
+    const uint32_t ft = (d12 & ((49u < re) ? 0xFF00u : 0u)) + ((d12 >> 16) & ((50u < re) ? 0xFFu : 0u));
+    const uint32_t fsub = isT ? ft : ((isU ? d10 : d9) & 0xFFFFu);
+    // pseudo-header (src, dst, proto, length) in the LE domain; ICMP has none
+    const uint32_t ph = bswap16(proto) + bswap16(L) + (d6 >> 16) + (d7 & 0xFFFFu) + (d7 >> 16) + (d8 & 0xFFFFu);
+    const uint32_t add = isI ? 0u : ph;
+    // over-counted: the LE word at 32 (l4 = 2 mod 4, sh keeps the parity) and the field bytes
+    const uint32_t sub = (d8 & 0xFFFFu) + fsub;
+    const uint32_t t = re - 1u;
+    const bool tail = (L & 1u) & ((t < fs) | (t >= fs + 2u));
+    const uint32_t st = ok ? (isT ? NFCS_ST_V4_TCP : (isU ? NFCS_ST_V4_UDP : NFCS_ST_V4_ICMP)) : NFCS_ST_V4_L4SKIP;
+    P.st = (isT | isU | isI) ? st : P.st;
+    P.flags |= ok ? (F_L4 | (isU ? F_UDP : 0u) | (tail ? F_TAIL : 0u)) : 0u;
+    P.rs = ok ? 34u + sh : P.rs;
+    P.re = ok ? re + sh : P.re;
+    P.fs = ok ? fs + sh : P.fs;
+    P.corr = ok ? add - sub : P.corr;
+    return P;
+}
+
 // Common headers with compile-time offsets: untagged / 802.1Q; IPv4 with IHL 5; IPv6; non-IP.
 // Returns F_SEQ in flags for everything else (IHL != 5: options, IHL < 5, past the frame).
 template <int R>
@@ -369,7 +410,7 @@ DEV RPlan fast_plan(const uint4& c0, uint32_t rowbase4, uint32_t len) {
         RPlan P = rplan_none(NFCS_ST_V4);
         P.flags = F_IP;
         P.ipw = (24u + sh) | (((~fold32(s)) & 0xFFFFu) << 16);
-        return fast_l4(V, P, lenv, 1u, 34u, V.b(23), sh);
+        return fast_l4_v4(V, P, lenv, V.b(23), sh);
     }
     // 741-765: effective EtherType (after one tag) must be IPv6 and the nibble 6
     const uint32_t et = (len >= 14 + sh) ? V.be16(12) : 0u;
@@ -820,19 +861,20 @@ DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             lc.w = sel ? v.w : lc.w;
         }
         if (own) {
-            const uint32_t o = 16u * last;
+            // the chunk's bytes at or past re come off again: dword j keeps its low
+            // clamp(8 (re - o) - 32 j, 0, 32) bits (one 64-bit shift each). Bytes under lo4 of a one-chunk
+            // region were never added, and none of them lies at or past re (re >= rs >= lo4).
+            const uint32_t o = 16u * last, kb8 = 8u * (re - o);
             uint32_t ex = 0;
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
-                const int nb = (int)re - (int)(o + 4u * j);
-                const uint32_t mk = nb >= 4 ? 0u : (nb <= 0 ? 0xFFFFFFFFu : ~((1u << (8 * nb)) - 1u));
-                // bytes under lo4 of a one-chunk region were never added
-                const uint32_t ml = (o + 4u * j >= lo4) ? 0xFFFFFFFFu : 0u;
-                ex = wsum(comp(lc, j) & mk & ml, ex);
+                const int s = min(max((int)kb8 - 32 * (int)j, 0), 32);
+                ex = wsum(comp(lc, j) & (uint32_t)(~0ull << s), ex);
             }
             acc -= ex;
-            const uint32_t t = re - 1u;
-            if (tailfix) acc += 255u * ((comp(lc, (t - o) >> 2) >> (8 * (t & 3u))) & 0xFFu);
+            const uint32_t t = re - 1u - o, q = t >> 2;
+            const uint32_t dt = q == 0 ? lc.x : (q == 1 ? lc.y : (q == 2 ? lc.z : lc.w));
+            if (tailfix) acc += 255u * ((dt >> (8 * (t & 3u))) & 0xFFu);
         }
     }
     // continuation batches for frames longer than R*K chunks (jumbo)
