@@ -446,12 +446,12 @@ int update_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfc
     return NFCS_OK;
 }
 
-// The fused L3 forward on stream st; a burst above kSubBatchAbovePackets defers the stores of its
-// long-frame waves through patch records in the context workspace (one per packet of a sub-batch).
+// The fused L3 forward on stream st; a burst above kFwdDeferAbovePackets defers the stores of its
+// long-frame waves through forward records in the context workspace (one per packet of a sub-batch).
 int l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const nfcs_desc* d_desc,
                       const uint32_t* d_nh, uint32_t n, const nfcs_nexthop* d_table, uint32_t table_n,
                       uint8_t* d_status, hipStream_t st) {
-    const bool dfr = n > nfcs::kSubBatchAbovePackets;
+    const bool dfr = n > nfcs::kFwdDeferAbovePackets;
     if (dfr) NFCS_HIP(acquire_ws(c, nfcs::kSubBatchPackets, st));
     const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
     NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,

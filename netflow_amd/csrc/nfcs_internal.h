@@ -52,6 +52,12 @@ constexpr uint32_t kInlineMaxPackets = 65536;
 // 16-19).
 constexpr uint32_t kSubBatchPackets = 1u << 19;
 constexpr uint32_t kSubBatchAbovePackets = 1u << 20;
+// The fused L3 forward on long frames defers its stores (read pass writing 8-byte forward records,
+// then apply_fwd_kernel per kSubBatchPackets sub-batch) for bursts of more than this many packets;
+// smaller bursts store their segments inline from one kernel. Round 4: in the steady state (calls
+// rotating over fresh batches) the inline write-through segments cost 1M-packet C1 bursts as much as
+// the update's inline stores do.
+constexpr uint32_t kFwdDeferAbovePackets = kInlineMaxPackets;
 // Below this mean arena footprint per packet the checksum kernel runs in one-wave workgroups at
 // 7 waves/SIMD (C3 +2-3%); the shape changes speed only, never the store form.
 constexpr uint64_t kSmallMeanBytes = 1200;

@@ -1382,12 +1382,12 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
                                                    nullptr, nullptr, fa);
         return hipGetLastError();
     }
-    if (ws && n > kSubBatchAbovePackets) {
-        // bursts of long frames larger than the memory-side cache: per 512K-packet sub-batch, a
-        // read pass whose long-frame waves write patch records instead of segments, then
-        // apply_fwd_kernel while the header lines are still cached (4M x 1500 B
-        // 0.681 -> 0.705; mixes like C3, whose waves rarely defer, lose 10% to the sub-batch
-        // launches and stay in one inline launch)
+    if (ws && n > kFwdDeferAbovePackets) {
+        // bursts of long frames: per 512K-packet sub-batch, a read pass whose long-frame waves write
+        // forward records instead of segments, then apply_fwd_kernel while the header lines are
+        // still in the memory-side cache (4M x 1500 B 0.681 -> 0.705; round 4, calls
+        // rotating over fresh batches: 1M C1 bursts too; mixes like C3, whose waves rarely defer,
+        // lose 10% to the sub-batch launches and take the short-mix shape above)
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
             const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};

@@ -112,13 +112,13 @@ def _pad_groups(frames, rng, keep_every=5):
     return out
 
 
-@pytest.mark.parametrize("align", [16, 128])
-def test_l3_long_frame_fuzz_vs_oracle(engine, align):
-    """A burst of 100K mostly long frames (the long-frame shape, 16-lane rows) with every header
-    kind of the fuzz (tagged, options, IHL < 5, IPv6, ICMP, expired TTLs, no route): bytes and
-    statuses against the oracle. (A deferred store form for such bursts was built and measured
-    slower; this test covered it too.)"""
-    n = 100_003  # ragged: the last group of 4 is partial
+@pytest.mark.parametrize("align,n", [(16, 100_003), (128, 100_003), (128, 60_001)])
+def test_l3_long_frame_fuzz_vs_oracle(engine, align, n):
+    """Bursts of mostly long frames (the long-frame shape, 16-lane rows) with every header kind of
+    the fuzz (tagged, options, IHL < 5, IPv6, ICMP, expired TTLs, no route): bytes and statuses
+    against the oracle. 100K packets take the deferred form (forward records + apply_fwd_kernel,
+    above kFwdDeferAbovePackets), 60K the inline segment stores; both end ragged (a partial last
+    group of 4)."""
     rng = np.random.default_rng(align + 7)
     frames, table, nh = random_l3_case(31 + align, n, table_n=8)
     frames = _pad_groups(frames, rng)
@@ -157,9 +157,9 @@ def test_l3_large_batch_vs_oracle(engine):
 
 
 def test_l3_deferred_sub_batches_fuzz_vs_oracle(engine):
-    """Above kSubBatchAbovePackets the forward defers the stores of its long-frame waves: per
-    512K-packet sub-batch, a read pass writing patch records, then apply_fwd_kernel re-reading and
-    writing back each forwarded packet's first 64 bytes. 1.2M mostly long fuzz frames (every header
+    """Above kFwdDeferAbovePackets (64K) the forward defers the stores of its long-frame waves: per
+    512K-packet sub-batch, a read pass writing 8-byte forward records, then apply_fwd_kernel writing
+    each forwarded packet's bytes from its record. 1.2M mostly long fuzz frames (every header
     kind, expired TTLs, no route, deferring and inline groups side by side, a partial last group):
     bytes and statuses against the oracle."""
     rng = np.random.default_rng(77)

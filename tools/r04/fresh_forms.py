@@ -15,6 +15,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 os.environ.setdefault("NFCS_LIB", os.path.join(HERE, "libnfcs_r4.so"))
 sys.path.insert(0, ROOT)
+if "--torch" in sys.argv:  # torch's bundled HIP runtime loaded first, as bench.py does (libnfcs binds to it)
+    import torch  # noqa: E402
+    torch.cuda.set_device(0)
+    torch.cuda.init()
 import netflow_amd as nf  # noqa: E402
 
 SEED = 20250620
@@ -40,6 +44,7 @@ def main():
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--modes", default="replay,rotate")
+    ap.add_argument("--torch", action="store_true", help="load torch's HIP runtime first (as bench.py)")
     a = ap.parse_args()
     L = nf.lib()
     fn = L.nfcs_r4_time
