@@ -85,9 +85,12 @@ def main():
         key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
             ("" if op == "update" else f"_{op}") + ("" if a.align == 128 else f"_align{a.align}")
         # launches per call: nfcs_update_device runs a long-frame batch of more than 1M packets
-        # as 512K-packet sub-batches (kSubBatchPackets), each its own read pass + write pass
-        # (the fused forward too, for long frames: read pass + apply_fwd_kernel per sub-batch)
-        sub = -(-P // (1 << 19)) if (op in ("update", "l3fwd") and P > (1 << 20)) else 1
+        # (kSubBatchAbovePackets) as 512K-packet sub-batches (kSubBatchPackets), each its own read
+        # pass + write pass; the fused forward does so for long-frame bursts of more than 64K
+        # (kFwdDeferAbovePackets, round 4): C1 = 2 sub-batches. Mixes (C3) run one kernel.
+        n_ = P or PACKETS[cfg]
+        above = {"update": 1 << 20, "l3fwd": 1 << 16}.get(op)
+        sub = -(-n_ // (1 << 19)) if (above and cfg in (1, 2) and n_ > above) else 1
         f = {k: v * sub for k, v in f.items()}
         w = {k: v * sub for k, v in w.items()}
         q = {k: v * sub for k, v in q.items()}
