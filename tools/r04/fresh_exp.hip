@@ -208,7 +208,8 @@ __global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* _
         RowStage<K> A, B;
         DescW<PW> DA = load_descw<PW>(desc, p0, n);
         DescW<PW> DB = load_descw<PW>(desc, p0 + PW, n);
-        row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), p0 + row, n, base16, rl);
+        row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), p0 + row, n, base16, rl,
+                                      wave_buf<PW>(DA, p0, n, arena, base16));
 #pragma unroll 1
         for (int g = 0; g < G; g += 2) {
             const uint64_t pa = p0 + (uint64_t)g * PW, pb = pa + PW;
@@ -218,13 +219,15 @@ __global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* _
                 break;
             }
             if (g + 2 < G) DA = load_descw<PW>(desc, pa + 2 * PW, n);
-            row_stage<K, R, false, false>(B, arena, arena_bytes, pick_desc<PW>(DB, row), pb + row, n, base16, rl);
+            row_stage<K, R, false, false>(B, arena, arena_bytes, pick_desc<PW>(DB, row), pb + row, n, base16, rl,
+                                          wave_buf<PW>(DB, pb, n, arena, base16));
             if (row_process<K, R, false, true, false, false, false, KCP>(A, rl, rowbase4, status, nullptr, true))
                 cold |= 1ull << g;
             const uint64_t pc = pb + PW;
             if (g + 2 < G && pc < n) {
                 if (g + 3 < G) DB = load_descw<PW>(desc, pc + PW, n);
-                row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), pc + row, n, base16, rl);
+                row_stage<K, R, false, false>(A, arena, arena_bytes, pick_desc<PW>(DA, row), pc + row, n, base16, rl,
+                                              wave_buf<PW>(DA, pc, n, arena, base16));
             }
             if (row_process<K, R, false, true, false, false, false, KCP>(B, rl, rowbase4, status, nullptr, true))
                 cold |= 1ull << (g + 1);
@@ -236,8 +239,9 @@ __global__ __launch_bounds__(64, OCC) void update_pipe_kernel(const nfcs_desc* _
         cold &= cold - 1;
         const uint64_t pg = p0 + (uint64_t)g * PW;
         RowStage<K> C;
-        row_stage<K, R, false, false>(C, arena, arena_bytes, pick_desc<PW>(load_descw<PW>(desc, pg, n), row), pg + row,
-                                      n, base16, rl);
+        const DescW<PW> DC = load_descw<PW>(desc, pg, n);
+        row_stage<K, R, false, false>(C, arena, arena_bytes, pick_desc<PW>(DC, row), pg + row, n, base16, rl,
+                                      wave_buf<PW>(DC, pg, n, arena, base16));
         row_process<K, R, false, true, false, false, true>(C, rl, rowbase4, status, nullptr, true);
     }
 }
