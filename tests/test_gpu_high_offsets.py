@@ -114,3 +114,44 @@ def test_flow_keys_past_32_gib(engine, big):
     assert np.array_equal(region(big, arena.nbytes), arena)  # read only
     for b in (d_desc, d_keys, d_hash):
         b.free()
+
+
+@pytest.mark.parametrize("slot", [0, 1536, 900, 256])
+def test_update_waves_spanning_32_gib(engine, big, slot):
+    """Rows of one wave with frames 32 GiB apart: even packets in a region at the arena's start,
+    odd ones in the region past 32 GiB, so every wave's frames span more than the 4 GB a per-wave
+    buffer resource addresses and its rows load through global addresses (row_stage's fallback);
+    the last wave is partial. Every launch shape (no hint: the long shape; slot hints: long, short,
+    tiny), bytes and statuses against the oracle, region by region, the guard untouched."""
+    frames = oracle.fuzz_frames(53, 0, 20001)
+    fa, fb = frames[0::2], frames[1::2]
+    arena_a, desc_a = oracle.pack_frames(fa, align=128)
+    arena_b, desc_b = oracle.pack_frames(fb, align=128)
+    ref_a, ref_b = arena_a.copy(), arena_b.copy()
+    st_a, _ = oracle.update_batch(ref_a, desc_a, nthreads=8)
+    st_b, _ = oracle.update_batch(ref_b, desc_b, nthreads=8)
+    lo = 4096
+    assert lo + arena_a.nbytes < BASE
+    big.upload(arena_a, lo)
+    big.upload(arena_b, BASE)
+    big.upload(np.full(GUARD, 0xA5, np.uint8), BASE + arena_b.nbytes)
+    n = len(frames)
+    desc = np.zeros(n, dtype=desc_a.dtype)
+    desc[0::2] = desc_a
+    desc[1::2] = desc_b
+    desc["off16"][0::2] = desc_a["off16"].astype(np.uint64) + lo // 16
+    desc["off16"][1::2] = desc_b["off16"].astype(np.uint64) + BASE // 16
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_st = engine.alloc(n)
+    try:
+        engine.set_slot_bytes(slot)
+        engine.update_device(big, BASE + arena_b.nbytes + GUARD, d_desc, n, d_st)
+        engine.sync()
+        st = d_st.download(np.uint8, n)
+        assert np.array_equal(st[0::2], st_a) and np.array_equal(st[1::2], st_b)
+        assert np.array_equal(big.download(np.uint8, arena_a.nbytes, lo), ref_a)
+        assert np.array_equal(region(big, arena_b.nbytes), ref_b)
+    finally:
+        engine.set_slot_bytes(0)
+        d_desc.free()
+        d_st.free()
