@@ -546,6 +546,7 @@ DEV uint32_t wave_max_rows(uint32_t x) {  // x row-uniform
 }
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kCpolNt = 2;  // buffer-load cache policy bits: nt (the global loads' non-temporal hint)
 
 template <int NT>
 DEV uint4 ld16(const uint4* p) {
@@ -628,6 +629,42 @@ DEV nfcs_desc pick_desc(const DescW<P>& D, uint32_t row) {  // mask selects: no 
     return d;
 }
 
+// The wave's frames as one raw buffer resource (round 4): based at the lowest frame of the wave's
+// rows (wave-uniform, from the descriptors in SGPRs), so a lane past its frame (or, in a line-aligned
+// window, before it) gives an out-of-range offset and its load returns zeros with no memory request.
+// With every such lane aimed at one shared zero chunk instead, up to half the load requests of a
+// short-frame batch went to a single 16-byte address, and C3 moved by 3% with the link-time address
+// of that chunk (profiles/r04_s2_zero_target_ab.jsonl). Used where it measured faster (rows_body's
+// BUF: the plain update's short shape). ok = every row's frame starts within
+// kBufSpan16 16-byte units of the base (32-bit offsets, a 64 KB frame on top); else row_stage loads
+// through global addresses, lanes past the frame from g_zero16.
+struct WaveBuf {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t lo16;
+    bool ok;
+};
+constexpr uint32_t kBufSpan16 = (1u << 28) - (1u << 13);
+constexpr uint32_t kBufOob = 0xFFFFFFF0u;  // num_records, and the offset of a lane past its frame
+
+template <int P>
+DEV WaveBuf wave_buf(const DescW<P>& D, uint64_t pw, uint32_t n, uint8_t* arena, uint32_t base16) {
+    uint32_t lo = D.w[0], hi = D.w[0];  // row 0 is always a packet (the wave exits when pw >= n)
+#pragma unroll
+    for (int i = 1; i < P; ++i) {
+        const uint32_t o = (pw + (uint64_t)i < n) ? D.w[2 * i] : D.w[0];
+        lo = min(lo, o);
+        hi = max(hi, o);
+    }
+    lo = rfl(lo);  // wave-uniform: a scalar branch in row_stage, not an exec-masked one
+    hi = rfl(hi);
+    WaveBuf b;
+    b.lo16 = lo;
+    b.ok = hi - lo < kBufSpan16;
+    b.rs = __builtin_amdgcn_make_buffer_rsrc(arena + ((int64_t)lo - (int64_t)base16) * 16, (short)0, kBufOob,
+                                             0x00020000);
+    return b;
+}
+
 // One row's packet, staged: frame window and its first K slots of chunks in flight.
 template <int K>
 struct RowStage {
@@ -668,17 +705,18 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
-// (evict-first). Every load is always issued — lanes past the frame read g_zero16 — so the waits
+// (evict-first). Every load is always issued — lanes past the frame give an out-of-range buffer
+// offset and read zeros (WaveBuf; g_zero16 where a wave's frames span more than 4 GB) — so the waits
 // are counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
 // R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
 // each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
-// frame's alignment; lanes before the frame start or past its end read g_zero16. Frame-relative
+// frame's alignment; lanes before the frame start or past its end read zeros. Frame-relative
 // windows on a frame that starts mid-line make every instruction touch one line more (densely
 // packed frames: C1 -4.5%, C2 -8%, C3 -15%; 64-byte-aligned starts C1 -5%;
 // profiles/r03_s3_ab_align*.jsonl). Without LA, mis = 0 and the windows are frame-relative.
-template <int K, int R = 16, bool FWD = false, bool LA = false>
+template <int K, int R = 16, bool FWD = false, bool LA = false, bool BUF = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, uint32_t nh = 0) {
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, uint32_t nh = 0) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     const bool bad = valid && ((d.off16 < base16) ||
@@ -693,11 +731,23 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
+    if (BUF && wb.ok) {  // wave-uniform
+        const uint32_t rel = (d.off16 - wb.lo16) * 16u;  // the row's frame in the wave's buffer
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t c = rl + (uint32_t)R * k - S.mis;  // frame chunk (wraps below the frame start)
-        const uint4* a = (c < nch) ? src + c : &g_zero16;
-        S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rl + (uint32_t)R * k - S.mis;  // frame chunk (wraps below the frame start)
+            const uint32_t vo = (c < nch) ? rel + 16u * c : kBufOob;
+            const u32x4_t t = k == 0 ? __builtin_amdgcn_raw_buffer_load_b128(wb.rs, vo, 0, 0)
+                                     : __builtin_amdgcn_raw_buffer_load_b128(wb.rs, vo, 0, kCpolNt);
+            S.v[k] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = rl + (uint32_t)R * k - S.mis;
+            const uint4* a = (c < nch) ? src + c : &g_zero16;
+            S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
+        }
     }
     // all K loads issue before any use of the header slot: without this fence the scheduler
     // hoists the forward decision's first DPP read above the last loads of the FWD kernel and
@@ -1042,7 +1092,14 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
     nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
     RowStage<K> S;
-    row_stage<K, R, FWD, LA>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl, 0u);
+    // buffer loads in the plain update's short shape (16-lane rows, one-wave workgroups), where most
+    // lanes of a wave's later slots are past their frames: C3 0.689-0.692 -> 0.664-0.669 ms per call;
+    // the long shape (+0.5%), the C4 shard (+0.8%), the 8-lane tiny shape (+1.2%) and the fused
+    // forward's short-mix shape (+4-10%) measured slower with them and keep global loads
+    // (profiles/r04_s2_wave_buf_ab.jsonl)
+    constexpr bool BUF = !FWD && BS == 64 && R == 16;
+    row_stage<K, R, FWD, LA, BUF>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl,
+                                  wave_buf<PW>(D, pw, n, arena, base16), 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
     if (FWD) {
 #pragma unroll
