@@ -705,9 +705,10 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
-// (evict-first). Every load is always issued — lanes past the frame give an out-of-range buffer
-// offset and read zeros (WaveBuf; g_zero16 where a wave's frames span more than 4 GB) — so the waits
-// are counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
+// (evict-first). Every load is always issued — lanes past the frame read zeros: from g_zero16, or
+// in the BUF shape (the update's short shape) through an out-of-range buffer offset with no memory
+// request (WaveBuf; g_zero16 again where a wave's frames span more than 4 GB) — so the waits are
+// counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
 // R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
 // each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
 // frame's alignment; lanes before the frame start or past its end read zeros. Frame-relative
