@@ -231,4 +231,14 @@ call_r() {
   done; done
 }
 
+call_s() {
+  # round 4 session 2, GPU call s: instructions per wave of the C3 short shape (the update) and the forward's
+  # C3 mix after the session's plan rewrite: SQ counters, one rocprofv3 pass each (kernel trace only)
+  mkdir -p gpurun_out/r4s && export TMPDIR=/tmp && \
+  for spec in "c3 --config 3" "fwdc3 --op l3fwd --config 3"; do
+    set -- $spec; name=$1; shift
+    timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES --kernel-trace --output-format csv -d "$PWD/gpurun_out/r4s/$name" -o p -- python3 bench.py "$@" --no-cpu --no-host --no-c4 --no-replay --steps 10 --warmup 1 > gpurun_out/r4s/$name.json 2> gpurun_out/r4s/$name.err || return 1
+  done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
