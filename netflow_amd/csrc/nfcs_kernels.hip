@@ -1445,11 +1445,14 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // forward records instead of segments, then apply_fwd_kernel while the header lines are
         // still in the memory-side cache (4M x 1500 B 0.681 -> 0.705; round 4, calls
         // rotating over fresh batches: 1M C1 bursts too; mixes like C3, whose waves rarely defer,
-        // lose 10% to the sub-batch launches and take the short-mix shape above)
+        // lose 10% to the sub-batch launches and take the short-mix shape above). The read pass is
+        // held at 6 waves/SIMD by kRowsLdsPad, as the update's long shape (round 4, calls rotating over
+        // fresh batches: 4M -0.9%, C1 -0.2% per call against 7; 5 waves +1.5-3.5%;
+        // profiles/r04_s2_fwd_occupancy_ab.jsonl)
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
             const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};
-            launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, 0u, stream, arena, arena_bytes, desc + i, m,
+            launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, kRowsLdsPad, stream, arena, arena_bytes, desc + i, m,
                                                           0u, status ? status + i : nullptr, nullptr, ws, fs);
             hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
                                desc + i, m, nh + i, table, (const nfcs_patch*)ws);

@@ -241,4 +241,43 @@ call_s() {
   done
 }
 
+call_t() {
+  # round 4 session 2, GPU call t: the fused forward's deferred read pass (bursts above 64K long frames) at 7
+  # waves/SIMD (the product) against 6 and 5 (unused dynamic LDS caps the workgroups per CU, as the update's
+  # long shape is held at 6): forward C1 and 4M, alternating on one box
+  mkdir -p gpurun_out/r4t && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_s2c prod_fwd6 prod_fwd5; do
+    for spec in "fwdc1 --op l3fwd --config 1" "fwd4m --op l3fwd --packets 4194304"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4t/${name}_${lib}_$r.json 2>> gpurun_out/r4t/bench.err || return 1
+    done
+  done; done
+}
+
+call_u() {
+  # round 4 session 2, GPU call u: the update's long shape at 7 waves/SIMD (21 KB of unused LDS per
+  # workgroup) against the product's 6, now that the steady state (rotation) is the measure — round 3's
+  # sweep chose 6 on the replayed form and noted fresh batches +1.5% at 7 — C1 and the C4 shard, alternating
+  mkdir -p gpurun_out/r4u && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_s2c prod_occ7; do
+    for spec in "c1 --config 1" "c4 --packets 4194304" "c2 --config 2"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4u/${name}_${lib}_$r.json 2>> gpurun_out/r4u/bench.err || return 1
+    done
+  done; done
+}
+
+call_v() {
+  # round 4 session 2, GPU call v: the final product (the forward's deferred read pass at 6 waves/SIMD):
+  # the whole GPU suite, smoke(), the default bench line, the forward lines (C1, 4M, C3 mix) and C3
+  mkdir -p gpurun_out/r4v && export TMPDIR=/tmp && \
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4v/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4v/smoke.log 2>&1 && \
+  timeout -k 10 400 python3 -u bench.py > gpurun_out/r4v/bench_default.json 2> gpurun_out/r4v/bench_default.err && \
+  for spec in "fwdc1 --op l3fwd --config 1" "fwd4m --op l3fwd --packets 4194304" "fwdc3 --op l3fwd --config 3" "c3 --config 3"; do
+    set -- $spec; name=$1; shift
+    timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 > gpurun_out/r4v/bench_$name.json 2>> gpurun_out/r4v/bench.err || return 1
+  done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
