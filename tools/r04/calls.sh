@@ -280,4 +280,17 @@ call_v() {
   done
 }
 
+call_w() {
+  # round 4 session 2, GPU call w: C1 as one read + write pass pair (the product) against two 512K sub-batches
+  # (kSubBatchAbovePackets 512K, libnfcs_prod_sb512): on some boxes C1 ran 2-3% below the C4 shard's 512K
+  # sub-batches in the same run; bench C1 alternating, then rocprofv3 kernel stats of both
+  mkdir -p gpurun_out/r4w && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_s2e prod_sb512; do
+    NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py --no-cpu --no-host --no-replay > gpurun_out/r4w/c1_${lib}_$r.json 2>> gpurun_out/r4w/bench.err || return 1
+  done; done && \
+  for lib in prod_s2e prod_sb512; do
+    NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r4w/prof_$lib" -o c1 -- python3 bench.py --no-cpu --no-host --no-replay --no-c4 --steps 40 > gpurun_out/r4w/prof_$lib.json 2> gpurun_out/r4w/prof_$lib.err || return 1
+  done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
