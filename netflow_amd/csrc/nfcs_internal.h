@@ -47,11 +47,13 @@ constexpr uint32_t kInlineMaxPackets = 65536;
 // of kSubBatchPackets (read pass, then write pass, per sub-batch): 512K header lines (64 MB,
 // 128 MB when frames straddle lines) stay in the 256 MB memory-side cache between the two passes.
 // On the 4M shard 512K and 1M sub-batches measured alike (0.749-0.755 / 0.749 against 0.683-0.714
-// in one launch), 2M 0.710; a 1M batch split in two measured within ±2% of one launch (C1
-// replayed and fresh, two boxes), so batches up to 1M stay one launch (tools/exp/ab.py variants
-// 16-19).
+// in one launch), 2M 0.710. Round 4, calls rotating over fresh batches (the steady state): C1 as two
+// 512K sub-batches 0.2591-0.2604 ms per call against 0.2596-0.2669 in one launch pair on two boxes
+// (rocprofv3: 2 x (116.8 + 13.1) against 231.0 + 30.0 us), and on the boxes where C1 in one pair ran
+// 2-3% below the 4M shard's 512K sub-batches in the same run, those held their rate: so every batch
+// above 512K long-frame packets is split (profiles/r04_s2_c1_sub_batches.jsonl).
 constexpr uint32_t kSubBatchPackets = 1u << 19;
-constexpr uint32_t kSubBatchAbovePackets = 1u << 20;
+constexpr uint32_t kSubBatchAbovePackets = 1u << 19;
 // The fused L3 forward on long frames defers its stores (read pass writing 8-byte forward records,
 // then apply_fwd_kernel per kSubBatchPackets sub-batch) for bursts of more than this many packets;
 // smaller bursts store their segments inline from one kernel. Round 4: in the steady state (calls

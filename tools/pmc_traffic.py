@@ -84,12 +84,12 @@ def main():
         wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P, a.align)
         key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
             ("" if op == "update" else f"_{op}") + ("" if a.align == 128 else f"_align{a.align}")
-        # launches per call: nfcs_update_device runs a long-frame batch of more than 1M packets
-        # (kSubBatchAbovePackets) as 512K-packet sub-batches (kSubBatchPackets), each its own read
+        # launches per call: nfcs_update_device runs a long-frame batch of more than 512K packets
+        # (kSubBatchAbovePackets; 1M before round 4 session 2) as 512K-packet sub-batches (kSubBatchPackets), each its own read
         # pass + write pass; the fused forward does so for long-frame bursts of more than 64K
         # (kFwdDeferAbovePackets, round 4): C1 = 2 sub-batches. Mixes (C3) run one kernel.
         n_ = P or PACKETS[cfg]
-        above = {"update": 1 << 20, "l3fwd": 1 << 16}.get(op)
+        above = {"update": 1 << 19, "l3fwd": 1 << 16}.get(op)
         sub = -(-n_ // (1 << 19)) if (above and cfg in (1, 2) and n_ > above) else 1
         f = {k: v * sub for k, v in f.items()}
         w = {k: v * sub for k, v in w.items()}

@@ -293,4 +293,21 @@ call_w() {
   done
 }
 
+call_x() {
+  # round 4 session 2, GPU call x: the product with long-frame batches split above 512K packets (C1 = two
+  # sub-batches): the whole GPU suite, smoke(), the default bench line, rocprofv3 kernel stats of C1
+  mkdir -p gpurun_out/r4x && export TMPDIR=/tmp && \
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4x/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4x/smoke.log 2>&1 && \
+  timeout -k 10 400 python3 -u bench.py > gpurun_out/r4x/bench_default.json 2> gpurun_out/r4x/bench_default.err && \
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r4x/prof_c1" -o c1 -- python3 bench.py --no-cpu --no-host --no-replay --no-c4 --steps 40 > gpurun_out/r4x/prof_c1.json 2> gpurun_out/r4x/prof_c1.err
+}
+
+call_y() {
+  # round 4 session 2, GPU call y: PMC traffic per call of C1 and C2 now that C1 runs as two 512K
+  # sub-batches (tools/pmc_traffic.py counts the sub-batches per call), merged into the committed record
+  mkdir -p gpurun_out/r4y && export TMPDIR=/tmp && \
+  timeout -k 10 600 python3 tools/pmc_traffic.py --out "$PWD/gpurun_out/r4y/pmc" --configs 1 --merge "$PWD/profiles/traffic.json" > gpurun_out/r4y/pmc.log 2>&1
+}
+
 "call_${1:?usage: calls.sh <letter>}"
