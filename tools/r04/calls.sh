@@ -310,4 +310,17 @@ call_y() {
   timeout -k 10 600 python3 tools/pmc_traffic.py --out "$PWD/gpurun_out/r4y/pmc" --configs 1 --merge "$PWD/profiles/traffic.json" > gpurun_out/r4y/pmc.log 2>&1
 }
 
+call_z() {
+  # round 4 session 2, GPU call z: jumbo frames' continuation batches double-buffered (batch b+1's loads in
+  # flight while b is summed; libnfcs_prod_dbuf, timing build: the long shape's registers rise to 85 VGPRs)
+  # against the product (libnfcs_prod_s2f): C2 and C1, alternating
+  mkdir -p gpurun_out/r4z && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_s2f prod_dbuf; do
+    for spec in "c2 --config 2" "c1 --config 1"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4z/${name}_${lib}_$r.json 2>> gpurun_out/r4z/bench.err || return 1
+    done
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
