@@ -71,8 +71,10 @@ constexpr uint64_t kTinyMeanBytes = 800;
 // past the caches (`sc0 sc1 nt`): 1M frames in 128-byte slots 177 vs 181 µs, in 384 / 640-byte
 // slots 212-216 vs 208 / 258 vs 245 µs, C1 0.698-0.704 vs 0.728-0.731.
 constexpr uint64_t kVlanWtMeanBytes = 256;
-// Dynamic LDS per 256-thread checksum workgroup (unused): 6 workgroups = 6 waves/SIMD per CU.
-constexpr unsigned kRowsLdsPad = 24576;
+// Dynamic LDS per 256-thread checksum workgroup (unused): 5 workgroups = 5 waves/SIMD per CU.
+constexpr unsigned kRowsLdsPad = 30720;
+// The same for 6 workgroups = 6 waves/SIMD: the forward's deferred read pass, the stream-read forms.
+constexpr unsigned kRowsLdsPad6 = 24576;
 
 // The mean arena bytes per packet that pick a launch shape (speed only): the context's slot-size
 // hint (nfcs_ctx_set_slot_bytes) when set, else arena_bytes / n.

@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
 //   kShapeShort  (< kSmallMeanBytes) 16-lane rows in one-wave workgroups at 7 waves/SIMD: mixes of
 //                short and long frames (C3), where 8-lane rows would need a second row pass for
 //                most waves (C3 -7.5%);
-//   kShapeLong   16-lane rows in 256-thread workgroups held at 6 waves/SIMD.
+//   kShapeLong   16-lane rows in 256-thread workgroups held at 5 waves/SIMD.
 enum : int { kShapeTiny = 0, kShapeShort = 1, kShapeLong = 2 };
 
 // One launch of update_rows_kernel (the grid size passed as `nblocks` too).
@@ -1391,9 +1391,11 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     // The short shape's one-wave workgroups at 7 waves/SIMD: short frames make short-lived waves,
     // and single-wave workgroups retire and relaunch them with less granularity loss (C3 +2-3%);
     // __launch_bounds__ 7 caps the kernel at 94 SGPRs (at the compiler's 106 the SGPR file admits
-    // only 6 waves/SIMD: C3 +2%). 256-thread workgroups are held at 6 waves/SIMD by kRowsLdsPad
-    // bytes of (unused) LDS: at the 8 their 54 VGPRs allow, the read stream runs slower (C1 0.768
-    // vs 0.777, the 4M shard 0.710 vs 0.718; 7 waves in between, 5 worse: tools/exp/occ_sweep.sh).
+    // only 6 waves/SIMD: C3 +2%). 256-thread workgroups are held at 5 waves/SIMD by kRowsLdsPad
+    // bytes of (unused) LDS: at the 8 their 54 VGPRs allow, the read stream runs slower (round 1,
+    // one replayed batch: C1 0.768 vs 0.777 at 6). Round 4, calls rotating over fresh batches with
+    // 512K-packet sub-batches: 5 waves beat 6 by 1.2-1.5% on C1, 1.6% on the C4 shard, 0.3% on C2
+    // (profiles/r04_s2_long_occupancy5_ab.jsonl).
     const uint64_t mean = shape_mean(arena_bytes, n, slot_bytes);
     const int shape = mean < kTinyMeanBytes ? kShapeTiny : (mean < kSmallMeanBytes ? kShapeShort : kShapeLong);
     // Long frames in a batch of more than kSubBatchAbovePackets: read pass and write pass alternate
@@ -1446,13 +1448,13 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // still in the memory-side cache (4M x 1500 B 0.681 -> 0.705; round 4, calls
         // rotating over fresh batches: 1M C1 bursts too; mixes like C3, whose waves rarely defer,
         // lose 10% to the sub-batch launches and take the short-mix shape above). The read pass is
-        // held at 6 waves/SIMD by kRowsLdsPad, as the update's long shape (round 4, calls rotating over
-        // fresh batches: 4M -0.9%, C1 -0.2% per call against 7; 5 waves +1.5-3.5%;
+        // held at 6 waves/SIMD by kRowsLdsPad6 (round 4, calls rotating over fresh batches: 4M -0.9%,
+        // C1 -0.2% per call against 7; 5 waves, the update's long shape, +1.5-3.5% here;
         // profiles/r04_s2_fwd_occupancy_ab.jsonl)
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
             const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};
-            launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, kRowsLdsPad, stream, arena, arena_bytes, desc + i, m,
+            launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, kRowsLdsPad6, stream, arena, arena_bytes, desc + i, m,
                                                           0u, status ? status + i : nullptr, nullptr, ws, fs);
             hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
                                desc + i, m, nh + i, table, (const nfcs_patch*)ws);
@@ -2057,9 +2059,9 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsi
     auto grid = [&](uint32_t k) { return dim3((uint32_t)((n16 + 64u * k * kWavesPerBlock - 1) / (64u * k * kWavesPerBlock))); };
     switch (form) {
     case 1: hipLaunchKernelGGL(stream_read_strided_kernel, dim3(512), dim3(kBlock), 0, stream, q, n16, sink); break;
-    // forms 0 and 2 are held at 6 waves/SIMD by kRowsLdsPad, as the checksum read pass is
-    case 0: hipLaunchKernelGGL((stream_read_kernel<6, true>), grid(6), dim3(kBlock), kRowsLdsPad, stream, q, n16, sink); break;
-    case 2: hipLaunchKernelGGL((stream_read_kernel<6, false>), grid(6), dim3(kBlock), kRowsLdsPad, stream, q, n16, sink); break;
+    // forms 0 and 2 are held at 6 waves/SIMD (the round-1 read stream's best)
+    case 0: hipLaunchKernelGGL((stream_read_kernel<6, true>), grid(6), dim3(kBlock), kRowsLdsPad6, stream, q, n16, sink); break;
+    case 2: hipLaunchKernelGGL((stream_read_kernel<6, false>), grid(6), dim3(kBlock), kRowsLdsPad6, stream, q, n16, sink); break;
     case 3: hipLaunchKernelGGL((stream_read_kernel<8, false>), grid(8), dim3(kBlock), 0, stream, q, n16, sink); break;
     case 4: hipLaunchKernelGGL((stream_read_kernel<16, false>), grid(16), dim3(kBlock), 0, stream, q, n16, sink); break;
     default: hipLaunchKernelGGL((stream_read_kernel<4, false>), grid(4), dim3(kBlock), 0, stream, q, n16, sink); break;
@@ -2069,7 +2071,7 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, int form, unsi
 
 // The read-only floor of the checksum read pass's own access pattern (bench `stream_ceiling`): the
 // batch's frames read exactly as update_rows_kernel reads them — 16-lane rows, 6 slots, four packets
-// per wave, 256-thread workgroups held at 6 waves/SIMD, XCD-aware order, the header slot with the
+// per wave, 256-thread workgroups held at 5 waves/SIMD, XCD-aware order, the header slot with the
 // default policy and the rest non-temporal, jumbo frames continued in batches of 6 slots — with
 // nothing computed or written (the chunks are XOR-ed into a value stored only if it equals an
 // impossible constant). A buffer stream reads the arena contiguously; this form reads what the

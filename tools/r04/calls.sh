@@ -323,4 +323,32 @@ call_z() {
   done; done
 }
 
+call_aa() {
+  # round 4 session 2, GPU call aa: why the double-buffered build (85 VGPRs in the long shape) ran C1 1.2%
+  # faster although C1 never enters the continuation loop: the product (6 waves/SIMD, LDS cap), the dbuf
+  # build and the product held at 5 waves/SIMD by LDS (libnfcs_prod_occ5): C1, the C4 shard, C2, alternating
+  mkdir -p gpurun_out/r4aa && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_s2f prod_dbuf prod_occ5; do
+    for spec in "c1 --config 1" "c4 --packets 4194304" "c2 --config 2"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4aa/${name}_${lib}_$r.json 2>> gpurun_out/r4aa/bench.err || return 1
+    done
+  done; done
+}
+
+call_ab() {
+  # round 4 session 2, GPU call ab: the product with the long shape at 5 waves/SIMD (forward's deferred
+  # read pass kept at 6): the whole GPU suite, smoke(), the default bench line, C2/C3/C4 shard and the
+  # forward lines, rocprofv3 kernel stats of C1
+  mkdir -p gpurun_out/r4ab && export TMPDIR=/tmp && \
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4ab/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4ab/smoke.log 2>&1 && \
+  timeout -k 10 400 python3 -u bench.py > gpurun_out/r4ab/bench_default.json 2> gpurun_out/r4ab/bench_default.err && \
+  for spec in "c2 --config 2" "c3 --config 3" "c4shard --packets 4194304" "l3fwd_c1 --op l3fwd" "l3fwd_4m --op l3fwd --packets 4194304"; do
+    set -- $spec; name=$1; shift
+    timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4ab/$name.json 2>> gpurun_out/r4ab/bench.err || return 1
+  done && \
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r4ab/prof_c1" -o c1 -- python3 bench.py --no-cpu --no-host --no-replay --no-c4 --steps 40 > gpurun_out/r4ab/prof_c1.json 2> gpurun_out/r4ab/prof_c1.err
+}
+
 "call_${1:?usage: calls.sh <letter>}"
