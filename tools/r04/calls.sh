@@ -351,4 +351,18 @@ call_ab() {
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r4ab/prof_c1" -o c1 -- python3 bench.py --no-cpu --no-host --no-replay --no-c4 --steps 40 > gpurun_out/r4ab/prof_c1.json 2> gpurun_out/r4ab/prof_c1.err
 }
 
+call_ac() {
+  # round 4 session 2, GPU call ac: each sub-batch's write pass on a second stream (event-ordered after its
+  # read pass), so it runs beside the next sub-batch's read pass; only the last write pass stays on the
+  # caller's stream. ovl512 / ovl256: 512K / 256K sub-batches, device-scope events; ovl512s: default
+  # (system-scope) events. Against the product (prod_f4): C1 and the C4 shard, alternating
+  mkdir -p gpurun_out/r4ac && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_f4 ovl512 ovl256 ovl512s; do
+    for spec in "c1 --config 1" "c4 --packets 4194304"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4ac/${name}_${lib}_$r.json 2>> gpurun_out/r4ac/bench.err || return 1
+    done
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
