@@ -365,4 +365,14 @@ call_ac() {
   done; done
 }
 
+call_ad() {
+  # round 4 session 2, GPU call ad: VLAN's long shape (127 VGPRs = 4 waves/SIMD) under __launch_bounds__
+  # 5 / 6 waves (96 / 80 VGPRs, 60 / 120 spilled to scratch; libnfcs_vlanw5 / w6) against the product:
+  # the VLAN bench line (C1 push/pop), alternating
+  mkdir -p gpurun_out/r4ad && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_f4 vlanw5 vlanw6; do
+    NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py --op vlan --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4ad/vlan_${lib}_$r.json 2>> gpurun_out/r4ad/bench.err || return 1
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
