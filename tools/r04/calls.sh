@@ -375,4 +375,15 @@ call_ad() {
   done; done
 }
 
+call_ae() {
+  # round 4 session 2, GPU call ae: VLAN's long shape with fewer continuation slots per batch (K2 = 2 / 3;
+  # C1's 1500-byte frames rarely continue) so that __launch_bounds__(256, 5) gives 5 waves/SIMD with few
+  # spills (K2 = 2: 96 VGPRs, 6 spilled; K2 = 3: 21 spilled), and K2 = 3 alone (112 VGPRs, 4 waves):
+  # against the product, the VLAN bench line, alternating
+  mkdir -p gpurun_out/r4ae && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_f4 vlan_k2lb5 vlan_k3lb5 vlan_k3; do
+    NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py --op vlan --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4ae/vlan_${lib}_$r.json 2>> gpurun_out/r4ae/bench.err || return 1
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
