@@ -386,4 +386,14 @@ call_ae() {
   done; done
 }
 
+call_af() {
+  # round 4 session 2, GPU call af: is the flow-key kernel occupancy-limited? Header rows of 80 instead of 96
+  # LDS bytes per packet (20 KiB per workgroup: 8 waves/SIMD instead of 6; timing probe only, headers
+  # past byte 79 are not staged: C1's untagged IPv4 frames need 38), against the product: flowkey, alternating
+  mkdir -p gpurun_out/r4af && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_f4 fk80; do
+    NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py --op flowkey --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4af/fk_${lib}_$r.json 2>> gpurun_out/r4af/bench.err || return 1
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
