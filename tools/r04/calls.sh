@@ -396,4 +396,13 @@ call_af() {
   done; done
 }
 
+call_ag() {
+  # round 4 session 2, GPU call ag: the final tree: smoke(), the default bench line, the 8-rank path
+  # rehearsed on this one GPU (every rank's C4 shard digest checked)
+  mkdir -p gpurun_out/r4ag && export TMPDIR=/tmp && \
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4ag/smoke.log 2>&1 && \
+  timeout -k 10 400 python3 -u bench.py > gpurun_out/r4ag/bench_default.json 2> gpurun_out/r4ag/bench_default.err && \
+  NFCS_BENCH_DEVICE=0 timeout -k 10 600 python3 -u bench.py --gpus 8 --steps 3 --warmup 1 > gpurun_out/r4ag/bench_gpus8_one_box.json 2> gpurun_out/r4ag/bench_gpus8.err
+}
+
 "call_${1:?usage: calls.sh <letter>}"
