@@ -405,4 +405,16 @@ call_ag() {
   NFCS_BENCH_DEVICE=0 timeout -k 10 600 python3 -u bench.py --gpus 8 --steps 3 --warmup 1 > gpurun_out/r4ag/bench_gpus8_one_box.json 2> gpurun_out/r4ag/bench_gpus8.err
 }
 
+call_ah() {
+  # round 4 session 2, GPU call ah: the long shape at 4 waves/SIMD (LDS pad 40960; libnfcs_occ4) against the
+  # product at 5 (libnfcs_prod_f5): C1, the C4 shard, C2, alternating
+  mkdir -p gpurun_out/r4ah && export TMPDIR=/tmp && \
+  for r in 1 2 3; do for lib in prod_f5 occ4; do
+    for spec in "c1 --config 1" "c4 --packets 4194304" "c2 --config 2"; do
+      set -- $spec; name=$1; shift
+      NFCS_LIB=tools/r04/libnfcs_$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay > gpurun_out/r4ah/${name}_${lib}_$r.json 2>> gpurun_out/r4ah/bench.err || return 1
+    done
+  done; done
+}
+
 "call_${1:?usage: calls.sh <letter>}"
