@@ -417,4 +417,10 @@ call_ah() {
   done; done
 }
 
+call_ai() {
+  # round 4 session 2, GPU call ai: the whole GPU suite on the final tree
+  mkdir -p gpurun_out/r4ai && export TMPDIR=/tmp && \
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4ai/pytest_gpu.log 2>&1
+}
+
 "call_${1:?usage: calls.sh <letter>}"
