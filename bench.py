@@ -13,8 +13,10 @@ Workloads (BASELINE.json configs):
   N = 1   config C1: 1M x 1500 B IPv4+UDP (configs[1]). The timed calls rotate over 4 separately
           generated batches (2 above 1M packets), so no call re-processes what the previous one just
           wrote (a NIC ring's steady state; --batches 1 replays one batch). The line also carries the
-          one-batch `replay` sub-line, the `c4_shard` sub-line (the per-GPU batch of N > 1) and the
-          `host` sub-line (the same frames in host memory through nfcs_update_host, PCIe included).
+          one-batch `replay` sub-line, the `c4_shard` sub-line (the per-GPU batch of N > 1), the
+          `c3` and `l3fwd_c3` sub-lines (config C3's 4M-frame mix through the update and the fused
+          forward) and the `host` sub-line (the same frames in host memory through nfcs_update_host,
+          PCIe included).
   N > 1   config C4: 32M x 1500 B sharded as independent 4M-packet batches, one per GPU (also at 2
           and 4 GPUs): per-GPU work fixed, scaling "weak". `--strong` instead splits ONE batch of
           the config's size across the ranks by bytes (nfcs_shard_bytes; e.g. the mixed C3), whose
@@ -421,6 +423,7 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-replay", action="store_true", help="skip the one-batch replay sub-line")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the C4-shard sub-line")
     ap.add_argument("--no-host", action="store_true", help="N = 1: skip the host-memory (PCIe) sub-line")
+    ap.add_argument("--no-mix", action="store_true", help="N = 1: skip the C3-mix sub-lines (update, fused forward)")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -752,8 +755,12 @@ def main():
         d_arena.free()
         d_arena = None
         out["c4_shard"] = c4_shard_line(eng, args)
+        if not args.no_mix:
+            out["c3"] = mix_line(eng, args, "update")
+            out["l3fwd_c3"] = mix_line(eng, args, "l3fwd")
         if not args.no_host:
             out["host"] = host_line(eng, args, n)
+            out["host_adapter"] = host_adapter_line(n)
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
@@ -860,6 +867,87 @@ def c4_shard_line(eng, args):
             "parity": {"digest": got, "reference_digest": want, "match": None if want is None else got == want}}
 
 
+def mix_line(eng, args, op: str):
+    """BASELINE C3 — 4M x U{64..1500} B IPv4 TCP/UDP, the length-divergence stress and the lines
+    furthest below roofline — as a sub-line of the N = 1 line, so the driver's clock covers it
+    (VERDICT r4 item 1): `op` "update" (nfcs_update_device, the short shape) or "l3fwd" (the fused
+    forward, switch.hpp:279-294, next hop i % 9, its short-mix shape). Calls rotate over 2 separately
+    generated batches (the steady state), warm-up, wall clock over the steps, HIP events on the
+    engine's stream around the rotated calls, the reference's digest of the result (configs.json
+    configs[3] / l3fwd_more) for both batches."""
+    n = DEFAULT_PACKETS[3]
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(3, SEED, 0, n, args.align)
+    batches = [(d_arena, nbytes, d_desc), eng.config_batch(3, SEED, 0, n, args.align)[:3]]
+    frame_bytes = float(hdesc["len"].astype(np.float64).sum())
+    ctr = [0]
+    extra = []
+    if op == "l3fwd":
+        g3 = golden()["l3fwd_c1"]
+        table = np.frombuffer(bytes.fromhex(g3["table"]), dtype=np.uint8).copy()
+        d_tab = eng.alloc(table.nbytes).upload(table)
+        d_nh = eng.alloc(4 * n).upload((np.arange(n) % 9).astype(np.uint32))
+        extra = [d_tab, d_nh]
+        algo_bytes = frame_bytes + 37.0 * n
+        want = next((g["digest_out"] for g in golden().get("l3fwd_more", [])
+                     if g["config"] == 3 and g["first"] == 0 and g["n"] == n), None)
+
+        def call(a, b, d):
+            eng.l3_forward_device(a, b, d, d_nh, n, d_tab, 8)
+
+        def regen():  # TTL 64: fresh frames before every timed region and before the parity call
+            for a, b, d in batches:
+                eng.gen_config_device(3, SEED, 0, n, a, b, d)
+            eng.sync()
+    else:
+        algo_bytes = frame_bytes + 12.0 * n
+        want = golden_digest(3, 0, n)
+        call = lambda a, b, d: eng.update_device(a, b, d, n)
+        regen = lambda: None
+
+    def step():
+        a, b, d = batches[ctr[0] % 2]
+        ctr[0] += 1
+        call(a, b, d)
+    steps = max(args.steps // 2, 10)
+    tw, done = time.perf_counter(), 0
+    while done < args.warmup or time.perf_counter() - tw < 0.3:
+        step()
+        done += 1
+        if done % 48 == 0:
+            regen()  # the forward: keep every warm-up call forwarding (TTL 64)
+    eng.sync()
+    regen()
+    dt = timed_steps(eng, step, steps) / steps
+    regen()
+    if op == "l3fwd":
+        ev_ms = event_ms(eng, step, steps) / steps
+        regen()
+        for a, b, d in batches:  # parity: one forward of each fresh batch
+            call(a, b, d)
+        eng.sync()
+    else:
+        ev_ms = eng.time_update_batches(batches, n, steps) / steps
+    rd_ms = eng.time_frames_read(d_arena, nbytes, d_desc, n, steps) / steps
+    digests = [f"{eng.digest_device(a, b, d, n, 0):016x}" for a, b, d in batches]
+    got = digests[0] if len(set(digests)) == 1 else "batches differ: " + ",".join(digests)
+    for a, _, d in batches:
+        a.free()
+        d.free()
+    for x in extra:
+        x.free()
+    achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
+    return {"workload": "C3: 4M x U{64..1500} B IPv4 TCP/UDP mix, device-resident"
+                        + (", fused L3 forward (next hop i % 9)" if op == "l3fwd" else ""),
+            "packets": n, "steps": steps, "batches_rotated": 2, "value": round(frame_bytes / dt / 1e9, 2),
+            "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+            "algorithmic_bytes_per_launch": int(algo_bytes),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frames_read_only_ms": round(rd_ms, 4),
+            "frames_read_only_GBps": round((frame_bytes + 8.0 * n) / (rd_ms * 1e-3) / 1e9, 1),
+            "frac_of_frames_read_only": round(achieved / ((frame_bytes + 8.0 * n) / (rd_ms * 1e-3) / 1e9), 4),
+            "parity": {"digest": got, "reference_digest": want, "match": None if want is None else got == want}}
+
+
 def replay_line(eng, args, first, n, algo_bytes, d_arena, nbytes, d_desc):
     """The same work REPLAYED on one batch (every call re-processes the frames the previous call
     wrote: their header lines are still in the memory-side cache, and the previous call's dirty
@@ -926,6 +1014,39 @@ def host_line(eng, args, n, reps: int = 3):
     node, local = eng.host_numa()
     out["gpu_numa_node"], out["staging_numa_local"] = node, local
     out["parity"] = {"reference_digest": want, "match": ok}
+    return out
+
+
+def host_adapter_line(n: int):
+    """The reference's own call convention end to end: C1's frames in n separately
+    allocated netflow::PacketBuffers (one `new[]` each, packet_buffer.hpp:21-31) as one burst of
+    netflow::Packet* through netflow_amd::update_checksums_batch (include/netflow_amd/netflow_adapter.hpp
+    -> nfcs_update_host_frames: gather into the pinned ring, H2D, GPU, checksum bytes written back in
+    place, pipelined); the same frames in netflow_amd::BufferPool slots of one pinned arena (no gather);
+    and the reference's per-packet Packet::update_checksums() over the same PacketBuffers on 1 and on
+    as many threads as the cgroup grants CPUs (16 at most) — wall clock per call, best and median of 3,
+    each result's digest against the reference's. Run by tests/cpp/_ref/netflow_adapter_test
+    `adapterbench` (compiled against the reference's headers by build(); it travels with the tree) as a
+    child process. Never `value`."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_ref", "netflow_adapter_test")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} missing (built by __graft_entry__.build() where /root/reference is)"}
+    quota = cgroup_cpu_quota()
+    threads = max(1, min(16, int(quota) if quota else len(allotted_cpus())))
+    want = golden_digest(1, 0, n) or ""
+    try:
+        r = subprocess.run([exe, "adapterbench", str(n), "3", str(threads), want], capture_output=True, text=True,
+                           timeout=300)
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        return {"error": repr(e)}
+    out["workload"] = (f"C1: {human(n)} x 1500 B IPv4+UDP, one netflow::PacketBuffer each (the reference's "
+                       "own classes), as one burst of netflow::Packet*")
+    out["timing"] = "wall clock per call, frames restored before each; best / median of 3"
+    out["rc"] = r.returncode
+    out["parity"] = {"reference_digest": want,
+                     "match": all(out.get(k, {}).get("match") for k in
+                                  ("adapter", "buffer_pool", "reference_1_thread", "reference_threads"))}
     return out
 
 

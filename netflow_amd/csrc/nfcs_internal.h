@@ -82,23 +82,31 @@ inline uint64_t shape_mean(uint64_t arena_bytes, uint32_t n, uint64_t slot_bytes
     return slot_bytes ? slot_bytes : arena_bytes / n;
 }
 
-// obs (optional, host-mapped): the launch samples its frames' mean footprint into *obs
-// (sample_footprint in nfcs_kernels.hip), for the next call's launch shape.
+// A footprint observation request (sample_footprint in nfcs_kernels.hip, for the next call's launch
+// shape): the host-mapped 64-bit slot the launch writes its sample to (null: none) and its tag — the
+// burst's generation in the high 32 bits (written back with the sample, so a late sample of an
+// earlier burst is told apart) and in the low 32 the packets to sample over: the whole call's n,
+// also when the call runs as sub-batches (the first one samples for all).
+struct ObsReq {
+    uint64_t* slot = nullptr;
+    uint64_t tag = 0;
+};
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
-                         uint64_t slot_bytes = 0, uint32_t* obs = nullptr);
+                         uint64_t slot_bytes = 0, ObsReq obs = {});
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
                              nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes = 0,
-                             uint32_t* obs = nullptr);
+                             ObsReq obs = {});
 
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
                        uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes = 0,
-                       uint32_t* obs = nullptr);
+                       ObsReq obs = {});
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,

@@ -48,7 +48,29 @@ DEV uint32_t xcd_block_n(uint32_t nblocks) {
 DEV uint32_t xcd_block() { return xcd_block_n(gridDim.x); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-__device__ uint4 g_zero16;  // target of the clamped loads of lanes past the frame end
+// Targets of the loads of lanes past their frame (or, in a line-aligned window, before it): every
+// load is issued by every lane, so a wave's compiler-counted vmcnt waits stay static. Round 5: a
+// pool of kZeroLines zero 128-byte lines, aligned to 4 KB, and each WAVE aims all such lanes at one
+// chunk of its own line (zero_chunk): one request per load instruction, as with one shared chunk,
+// but the waves' requests spread over every L2 channel. Round 4 aimed every lane of the chip at one
+// 16-byte global; its channel took up to half the load requests of a short-frame batch, and the
+// fused forward's C3 mix moved between 0.68 and 0.75 ms per call with that global's link-time address
+// and from run to run (profiles/r04_s2_zero_target_ab.jsonl; round 5: profiles/r05_zero_pool_ab.jsonl).
+constexpr uint32_t kZeroLines = 512;
+#ifdef NFCS_DATA_PAD
+__device__ __attribute__((used)) uint8_t g_data_pad[NFCS_DATA_PAD];
+#endif
+__device__ __attribute__((aligned(4096))) uint4 g_zero_pool[kZeroLines * 8];
+#ifndef NFCS_ZMODE
+#define NFCS_ZMODE 2
+#endif
+#ifndef NFCS_ZSTRIDE
+#define NFCS_ZSTRIDE 8
+#endif
+DEV const uint4* zero_chunk(uint64_t wave) {
+    return (NFCS_ZMODE & 1) ? g_zero_pool + ((uint32_t)wave & (kZeroLines - 1u)) * 8u : g_zero_pool;
+}
+DEV const uint4* zslot(const uint4* zl, int k) { return (NFCS_ZMODE & 2) ? zl + ((k * NFCS_ZSTRIDE) & (kZeroLines * 8 - 1)) : zl; }
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
 DEV uint32_t comp(const uint4& v, uint32_t j) {
@@ -637,7 +659,7 @@ DEV nfcs_desc pick_desc(const DescW<P>& D, uint32_t row) {  // mask selects: no 
 // of that chunk (profiles/r04_s2_zero_target_ab.jsonl). Used where it measured faster (rows_body's
 // BUF: the plain update's short shape). ok = every row's frame starts within
 // kBufSpan16 16-byte units of the base (32-bit offsets, a 64 KB frame on top); else row_stage loads
-// through global addresses, lanes past the frame from g_zero16.
+// through global addresses, lanes past the frame from the wave's zero chunk.
 struct WaveBuf {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t lo16;
@@ -675,6 +697,7 @@ struct RowStage {
     uint32_t valid, bad;
     uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
     uint32_t mis;   // 16-byte chunks between the frame start and the 128-byte line below it
+    const uint4* zl;  // the wave's zero chunk (zero_chunk): continuation loads past the frame
 };
 
 // Per-launch extras of update_rows_kernel: the fused L3 forward's inputs (unused by the plain
@@ -683,14 +706,18 @@ struct FwdArgs {
     const uint32_t* nh;
     const nfcs_nexthop* table;
     uint32_t table_n;
-    uint32_t* obs;
+    ObsReq obs;
 };
 
-// The mean footprint of a call's frames — 256 descriptors spread evenly over the batch, each length
-// rounded up to 128 bytes — written to *obs (host-mapped, system scope) by one wave of the launch.
-// The next call on the same descriptor array picks its launch shape from it when arena_bytes / n
-// cannot tell (a burst inside a larger ring; nfcs_api.hip update_device). Speed only.
-DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32_t lane, uint32_t* obs) {
+// The mean footprint of a call's frames — 256 descriptors spread evenly over the call's tag & 0xFFFFFFFF
+// packets from desc (the whole call, also when it runs as sub-batches: the first sub-batch samples),
+// each length rounded up to 128 bytes — written to *obs (host-mapped, system scope) by one wave of the
+// launch, in one 64-bit store together with the burst's generation (tag >> 32), so the host can tell
+// a late sample of an earlier burst from this one's. The next call over the same burst (descriptor
+// array, n and arena_bytes) picks its launch shape from it when arena_bytes / n cannot tell (a burst
+// inside a larger ring; nfcs_api.hip launch_shape). Speed only.
+DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint32_t lane, uint64_t* obs) {
+    const uint32_t n = (uint32_t)tag;
     uint32_t s = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
@@ -700,14 +727,16 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32
     s = row_sum<16>(s);
     const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)s, 0) + (uint32_t)__builtin_amdgcn_readlane((int)s, 16) +
                        (uint32_t)__builtin_amdgcn_readlane((int)s, 32) + (uint32_t)__builtin_amdgcn_readlane((int)s, 48);
-    if (lane == 0) __hip_atomic_store(obs, (t >> 8) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0)
+        __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | ((t >> 8) | 1u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
-// (evict-first). Every load is always issued — lanes past the frame read zeros: from g_zero16, or
-// in the BUF shape (the update's short shape) through an out-of-range buffer offset with no memory
-// request (WaveBuf; g_zero16 again where a wave's frames span more than 4 GB) — so the waits are
+// (evict-first). Every load is always issued — lanes past the frame read zeros: from the wave's zero
+// chunk zl, or in the BUF shape (the update's short shape) through an out-of-range buffer offset with
+// no memory request (WaveBuf; zl again where a wave's frames span more than 4 GB) — so the waits are
 // counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
 // R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
 // each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
@@ -717,7 +746,8 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint32_t n, uint32
 // profiles/r03_s3_ab_align*.jsonl). Without LA, mis = 0 and the windows are frame-relative.
 template <int K, int R = 16, bool FWD = false, bool LA = false, bool BUF = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, uint32_t nh = 0) {
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, const uint4* zl,
+                   uint32_t nh = 0) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     const bool bad = valid && ((d.off16 < base16) ||
@@ -729,6 +759,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     S.len = live ? d.len : 0u;
     S.frame = arena + (live ? off : 0);
     S.mis = LA && live ? (uint32_t)(((uintptr_t)S.frame >> 4) & 7u) : 0u;
+    S.zl = zl;
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
@@ -746,7 +777,7 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k - S.mis;
-            const uint4* a = (c < nch) ? src + c : &g_zero16;
+            const uint4* a = (c < nch) ? src + c : zslot(zl, k);
             S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
         }
     }
@@ -809,12 +840,11 @@ DEV uint4 hdr_view(const RowStage<K>& S, uint32_t rowbase4, uint32_t rl) {
     return a < (uint32_t)R ? r0 : r1;
 }
 
-// COLD = false: rows with an uncommon header are left alone (nothing stored for them) and the call
-// returns true when the wave has any, for the caller to run them later with COLD = true.
-// KC: slots per continuation batch of frames longer than R*K chunks (fewer: fewer live registers).
-template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false,
-          bool COLD = true, int KC = K>
-DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
+// (Round 4's measurement-only knobs — uncommon-header rows deferred to a later pass, fewer
+// continuation slots — were measured, not adopted, and dropped from the product; tools/r04/fresh_exp.hip
+// builds against the round-4 sources, git 00f5686.)
+template <int K, int R = 16, bool FWD = false, bool NT = false, bool DFR = false, bool LA = false>
+DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8_t* status,
                      nfcs_patch* rec, bool frame_stores, uint32_t table_n = 0,
                      const uint32_t* wmac = nullptr, const nfcs_nexthop* table = nullptr) {
     const uint32_t len = S.len;
@@ -930,15 +960,15 @@ DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     }
     // continuation batches for frames longer than R*K chunks (jumbo)
     const uint32_t cmax = wave_max_rows<R>(LA ? nre + S.mis : nre);
-    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * KC) {
-        uint4 w[KC];
+    for (uint32_t cb = (uint32_t)R * K; cb < cmax; cb += (uint32_t)R * K) {
+        uint4 w[K];
 #pragma unroll
-        for (int k = 0; k < KC; ++k) {
+        for (int k = 0; k < K; ++k) {
             const uint32_t c = cb + rlv + (uint32_t)R * k - S.mis;
-            w[k] = ld16<1>((c < nre) ? src + c : &g_zero16);
+            w[k] = ld16<1>((c < nre) ? src + c : zslot(S.zl, k));
         }
 #pragma unroll
-        for (int k = 0; k < KC; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
+        for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
     }
     const uint32_t z = row_sum<R>(acc) + P.corr;
     if (P.flags & F_L4) {
@@ -996,7 +1026,6 @@ DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     } else {
         emit(S.valid && !slow, st, ipw, l4w, frame_stores);
     }
-    if (!COLD) return __builtin_amdgcn_ballot_w64(slow) != 0;
     if (__builtin_amdgcn_ballot_w64(slow) != 0) {  // cold path, wave-uniform branch
         // Uncommon headers, handled last so that only the frame address and length are live
         // across the calls: the row's lane 0 parses from memory (IHL < 5 overlaps run the
@@ -1069,7 +1098,6 @@ DEV bool row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
         // the forward stored everything of an uncommon header here: nothing left for the write pass
         if (FWD && DFR && rec && slow && rl == 0) ((uint2*)rec)[S.p] = make_uint2(0xFFFFFFFFu, 0u);
     }
-    return false;
 }
 
 // One wave = 64/R packet rows; one workgroup per BS/R packets, as many workgroups as the batch
@@ -1100,7 +1128,7 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     // (profiles/r04_s2_wave_buf_ab.jsonl)
     constexpr bool BUF = !FWD && BS == 64 && R == 16;
     row_stage<K, R, FWD, LA, BUF>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl,
-                                  wave_buf<PW>(D, pw, n, arena, base16), 0u);
+                                  wave_buf<PW>(D, pw, n, arena, base16), zero_chunk(pw / PW), 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
     if (FWD) {
 #pragma unroll
@@ -1110,7 +1138,7 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
         if (!(SF == SF_DEFER && defer)) {
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) {
-                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)&g_zero16;
+                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)g_zero_pool;
                 wmac[3 * i] = m[0];
                 wmac[3 * i + 1] = m[1];
                 wmac[3 * i + 2] = m[2];
@@ -1131,18 +1159,18 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* _
                                                               uint32_t nblocks, uint8_t* __restrict__ arena,
                                                               uint64_t arena_bytes, uint32_t base16,
                                                               const uint32_t* __restrict__ nh,
-                                                              uint32_t* __restrict__ obs,
+                                                              uint64_t* __restrict__ obs,
                                                               uint8_t* __restrict__ status,
                                                               nfcs_patch* __restrict__ patch,
                                                               nfcs_patch* __restrict__ ws,
                                                               const nfcs_nexthop* __restrict__ table,
-                                                              uint32_t table_n) {
+                                                              uint32_t table_n, uint64_t obs_tag) {
     constexpr uint32_t PW = 64 / R;  // packets per wave
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
     const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
     const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (BS / R) + rfl(threadIdx.x >> 6) * PW;
     if (pw >= n) return;
-    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, n, lane, obs);
+    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, obs_tag, lane, obs);
     // the wave's PW descriptors: one scalar load (s_load_dwordx8 for PW = 4)
     const DescW<PW> D = load_descw<PW>(desc, pw, n);
     // the store form of each aligned group of 4 packets, from their own frame lengths (scalar
@@ -1333,14 +1361,15 @@ static void launch_rows(uint32_t grid, unsigned lds, hipStream_t stream, uint8_t
                         const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status, nfcs_patch* patch,
                         nfcs_patch* ws, const FwdArgs& fa) {
     hipLaunchKernelGGL((update_rows_kernel<K, R, OCC, BS, FWD, SF, LAM, KL>), dim3(grid), dim3(BS), lds, stream, desc, n, grid,
-                       arena, arena_bytes, base16, fa.nh, fa.obs, status, patch, ws, fa.table, fa.table_n);
+                       arena, arena_bytes, base16, fa.nh, fa.obs.slot, status, patch, ws, fa.table, fa.table_n,
+                       fa.obs.tag);
 }
 
 // One launch of the checksum path (its read pass and, for kUpdateAuto, its write pass) over n
 // packets, in the shape chosen for the whole call.
 static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
                                     uint32_t base16, uint8_t* status, nfcs_patch* patch, nfcs_patch* ws,
-                                    int form, int shape, hipStream_t stream, uint32_t* obs) {
+                                    int form, int shape, hipStream_t stream, ObsReq obs) {
     const FwdArgs nofwd = {nullptr, nullptr, 0, obs};
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
@@ -1383,7 +1412,7 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
-                         uint64_t slot_bytes, uint32_t* obs) {
+                         uint64_t slot_bytes, ObsReq obs) {
     (void)di;
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
@@ -1409,7 +1438,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
             const hipError_t e = launch_update_one(arena, arena_bytes, desc + i, std::min(kSubBatchPackets, n - i),
                                                    base16, status ? status + i : nullptr,
                                                    patch ? patch + i : nullptr, ws, form, shape, stream,
-                                                   i == 0 ? obs : nullptr);
+                                                   i == 0 ? obs : ObsReq{});
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
@@ -1420,7 +1449,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,
                              const nfcs_nexthop* table, uint32_t table_n, uint8_t* status,
-                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes, uint32_t* obs) {
+                             nfcs_patch* ws, hipStream_t stream, uint64_t slot_bytes, ObsReq obs) {
     (void)di;
     if (n == 0) return hipSuccess;
     const FwdArgs fa = {nh, table, table_n, obs};
@@ -1453,7 +1482,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // profiles/r04_s2_fwd_occupancy_ab.jsonl)
         for (uint32_t i = 0; i < n; i += kSubBatchPackets) {
             const uint32_t m = std::min(kSubBatchPackets, n - i);
-            const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : nullptr};
+            const FwdArgs fs = {nh + i, table, table_n, i == 0 ? obs : ObsReq{}};
             launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>((m + 15u) / 16u, kRowsLdsPad6, stream, arena, arena_bytes, desc + i, m,
                                                           0u, status ? status + i : nullptr, nullptr, ws, fs);
             hipLaunchKernelGGL(apply_fwd_kernel, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, arena,
@@ -1588,7 +1617,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
                                                            const uint32_t* __restrict__ caps,
                                                            uint32_t cap_all,
                                                            uint8_t* __restrict__ status,
-                                                           uint32_t* __restrict__ obs) {
+                                                           uint64_t* __restrict__ obs, uint64_t obs_tag) {
     static_assert(R == 16 || R == 8, "16- or 8-lane rows");
     constexpr uint32_t PW = 64 / R, KR = (uint32_t)(K * R);
     const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
@@ -1597,7 +1626,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     if (pw >= n) return;
     // the footprint sample for the next call's shape (lengths other waves are editing may be read
     // old or new: speed only)
-    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, n, lane, obs);
+    if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, obs_tag, lane, obs);
     const nfcs_desc d = pick_desc<PW>(load_descw<PW>(desc, pw, n), row);
     uint32_t op = op_all, cap = cap_all;
     {  // the wave's edit words / capacities: scalar loads, like the descriptors
@@ -1628,14 +1657,15 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     const uint32_t mis = (nl + lm <= KR || nl > KR) ? lm : 0u;
     const bool rot = LA && __builtin_amdgcn_ballot_w64(mis != 0) != 0;  // wave-uniform
 
+    const uint4* zl = zero_chunk(pw / PW);
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k - mis;  // frame chunk (wraps below the frame start)
-        v[k] = ld16<0>((c < nl) ? src + c : &g_zero16);
+        v[k] = ld16<0>((c < nl) ? src + c : zslot(zl, k));
     }
     // pop: the old dword after batch 0 (first dword of the window's chunk KR)
-    const uint32_t nx0 = *(const uint32_t*)((KR - mis < nl) ? src + (KR - mis) : &g_zero16);
+    const uint32_t nx0 = *(const uint32_t*)((KR - mis < nl) ? src + (KR - mis) : zl);
 
     // the edit the reference makes (packet.hpp:655-720), decided on the old header
     const RowHdr<R> h{rot ? vlan_view<K, R>(v, rowbase4, rl, mis) : v[0], rowbase4};
@@ -1730,9 +1760,9 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k - mis;
-                w[k] = ld16<1>((c < nl) ? src + c : &g_zero16);
+                w[k] = ld16<1>((c < nl) ? src + c : zslot(zl, k));
             }
-            const uint32_t nx = *(const uint32_t*)((cb + KR2 - mis < nl) ? src + (cb + KR2 - mis) : &g_zero16);
+            const uint32_t nx = *(const uint32_t*)((cb + KR2 - mis < nl) ? src + (cb + KR2 - mis) : zl);
             vlan_edit<K2, R>(e, w, mode, rl, false, carry, nx, 0u, cb, wend, mis);
             carry = row_bcast<R - 1, R>(w[K2 - 1].w);
 #pragma unroll
@@ -1801,7 +1831,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
                        uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes,
-                       uint32_t* obs) {
+                       ObsReq obs) {
     (void)di;
     if (n == 0) return hipSuccess;
     // Long frames continue in batches of 6 slots (128 VGPRs, 4 waves/SIMD); batches of 2 slots
@@ -1815,13 +1845,13 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
     const dim3 g8((n + 31u) / 32u), g16((n + 15u) / 16u);
     if (mean < kVlanWtMeanBytes)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_WT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status, obs);
+                           desc, n, ops, op_all, caps, cap_all, status, obs.slot, obs.tag);
     else if (mean < kTinyMeanBytes)
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status, obs);
+                           desc, n, ops, op_all, caps, cap_all, status, obs.slot, obs.tag);
     else  // 4 rows per wave, 4 waves per workgroup
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 16, true>), g16, dim3(kBlock), 0, stream, arena, arena_bytes,
-                           desc, n, ops, op_all, caps, cap_all, status, obs);
+                           desc, n, ops, op_all, caps, cap_all, status, obs.slot, obs.tag);
     return hipGetLastError();
 }
 
@@ -1869,6 +1899,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
     // line instead of two; round 3). Headers reaching past byte 47 (IPv6, IPv4 options) load chunks
     // 3..5 afterwards, lane by lane.
     const uint32_t rl = lane & 7u, r = lane >> 3;
+    const uint4* zl = zero_chunk(p0 / 64u);
     uint4 c[8];
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
@@ -1876,7 +1907,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
         const uint32_t qo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)dl.x);
         const uint32_t ql = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)len);
         const uint4* src = (const uint4*)(arena + (uint64_t)qo * 16u);
-        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : &g_zero16);
+        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : zslot(zl, (int)k));
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k)
@@ -1895,7 +1926,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
             if (more) {
                 const uint4* src = (const uint4*)(arena + off);
 #pragma unroll
-                for (uint32_t j = 3; j < 6; ++j) *(uint4*)(b + 16u * j) = ld16<0>(16u * j < len ? src + j : &g_zero16);
+                for (uint32_t j = 3; j < 6; ++j) *(uint4*)(b + 16u * j) = ld16<0>(16u * j < len ? src + j : zl);
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
@@ -2022,7 +2053,7 @@ __global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __rest
 #pragma unroll
     for (uint32_t k = 0; k < K; ++k) {
         const uint64_t i = base + 64u * k;
-        const uint4* a = i < n16 ? p + i : &g_zero16;
+        const uint4* a = i < n16 ? p + i : zero_chunk(w);
         v[k] = (MIX && k == 0) ? ld16<0>(a) : ld16<1>(a);
     }
     uint32_t acc = 0;
@@ -2089,11 +2120,12 @@ __global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __
     const bool live = pw + row < n && off + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes;
     const uint32_t nch = live ? (d.len + 15u) >> 4 : 0u;
     const uint4* src = (const uint4*)(arena + (live ? off : 0));
+    const uint4* zl = zero_chunk(pw / PW);
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k;
-        v[k] = k == 0 ? ld16<0>((c < nch) ? src + c : &g_zero16) : ld16<1>((c < nch) ? src + c : &g_zero16);
+        v[k] = k == 0 ? ld16<0>((c < nch) ? src + c : zslot(zl, k)) : ld16<1>((c < nch) ? src + c : zslot(zl, k));
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -2104,7 +2136,7 @@ __global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = cb + rl + (uint32_t)R * k;
-            w[k] = ld16<1>((c < nch) ? src + c : &g_zero16);
+            w[k] = ld16<1>((c < nch) ? src + c : zslot(zl, k));
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) acc ^= w[k].x ^ w[k].y ^ w[k].z ^ w[k].w;

@@ -33,9 +33,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <functional>
 #include <iostream>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "netflow_amd/netflow_adapter.hpp"
@@ -582,10 +584,156 @@ int cpubench_mode(size_t len, size_t n, size_t reps) {
     return bad ? 1 : 0;
 }
 
+// The reference's own call convention, end to end: n BASELINE C1 frames (the
+// seeded generator, nfcs_gen_config_device) in n separately allocated netflow::PacketBuffers — one
+// `new[]` each, 32 bytes of headroom, as BufferPool::allocate_buffer hands them out
+// (packet_buffer.hpp:21-31, buffer_pool.hpp:57-94) — checksummed as one burst of netflow::Packet* by
+// netflow_amd::update_checksums_batch (netflow_adapter.hpp: frames gathered into the pinned ring, H2D,
+// GPU, checksum bytes written back in place; what a caller of switch.hpp:294 that batches its burst
+// runs); the same frames in netflow_amd::BufferPool slots of one pinned arena (no gather); and the
+// reference's per-packet Packet::update_checksums() over the same PacketBuffers on 1 and on `threads`
+// host threads. Wall clock per call, frames restored before each; best and median of `reps`. Each
+// result's order-independent digest is compared with `want` (the reference's digest
+// of C1, tests/golden/configs.json). Prints one JSON line.
+int adapterbench_mode(size_t n, size_t reps, size_t threads, const std::string& want) {
+    using clk = std::chrono::steady_clock;
+    if (threads < 1) threads = 1;
+    int rc = NFCS_OK;
+    netflow_amd::ChecksumEngine* eng = netflow_amd::ChecksumEngine::try_instance(&rc);
+    if (!eng) {
+        std::printf("{\"error\": \"no engine: %s\"}\n", nfcs_strerror(rc));
+        return 1;
+    }
+    nfcs_ctx* c = eng->ctx();
+    // the frames: BASELINE C1, 16-byte aligned back to back, generated on the device
+    std::vector<nfcs_desc> desc(n);
+    uint64_t bytes = 0;
+    if (nfcs_layout_config(NFCS_CFG_C1_1500B_UDP, 20250620ull, 0, (uint32_t)n, 16, desc.data(), &bytes)) return 1;
+    void *d_arena = nullptr, *d_desc = nullptr;
+    if (nfcs_device_alloc(c, bytes, &d_arena) || nfcs_device_alloc(c, n * sizeof(nfcs_desc), &d_desc)) return 1;
+    if (nfcs_memcpy_h2d(c, d_desc, desc.data(), n * sizeof(nfcs_desc))) return 1;
+    if (nfcs_gen_config_device(c, NFCS_CFG_C1_1500B_UDP, 20250620ull, 0, (uint32_t)n, (uint8_t*)d_arena, bytes,
+                               (nfcs_desc*)d_desc, nullptr) || nfcs_stream_sync(c, nullptr))
+        return 1;
+    std::vector<uint8_t> pristine(bytes);
+    if (nfcs_memcpy_d2h(c, pristine.data(), d_arena, bytes)) return 1;
+    double frame_bytes = 0;
+    for (size_t i = 0; i < n; ++i) frame_bytes += desc[i].len;
+
+    auto parallel = [&](size_t k, const std::function<void(size_t, size_t)>& f) {  // f(i0, i1) over k threads
+        std::vector<std::thread> th;
+        for (size_t t = 1; t < k; ++t) th.emplace_back(f, n * t / k, n * (t + 1) / k);
+        f(0, n / k);
+        for (auto& x : th) x.join();
+    };
+    // digest of the frames as they are now in their buffers: gathered into the generator's layout
+    std::vector<uint8_t> img(bytes);
+    auto digest = [&](const std::function<const uint8_t*(size_t)>& data) -> std::string {
+        parallel(threads, [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i) std::memcpy(img.data() + (size_t)desc[i].off16 * 16, data(i), desc[i].len);
+        });
+        uint64_t d = 0;
+        if (nfcs_memcpy_h2d(c, d_arena, img.data(), bytes) ||
+            nfcs_digest_device(c, (uint8_t*)d_arena, bytes, (nfcs_desc*)d_desc, (uint32_t)n, 0, &d, nullptr))
+            return "error";
+        char s[32];
+        std::snprintf(s, sizeof(s), "%016llx", (unsigned long long)d);
+        return s;
+    };
+    struct Timing { std::vector<double> s; std::string digest; };
+    auto stats = [&](const Timing& t) {
+        std::vector<double> v = t.s;
+        std::sort(v.begin(), v.end());
+        char o[320];
+        std::snprintf(o, sizeof(o), "{\"GBps\": %.2f, \"GBps_median\": %.2f, \"ms_per_call\": %.3f, \"digest\": \"%s\", \"match\": %s}",
+                      frame_bytes / v[0] / 1e9, frame_bytes / v[v.size() / 2] / 1e9, v[0] * 1e3, t.digest.c_str(),
+                      t.digest == want ? "true" : "false");
+        return std::string(o);
+    };
+
+    // the reference's PacketBuffers and Packets, one heap buffer each
+    std::vector<std::unique_ptr<netflow::PacketBuffer>> rb(n);
+    std::vector<std::unique_ptr<netflow::Packet>> rp(n);
+    std::vector<netflow::Packet*> ptrs(n);
+    for (size_t i = 0; i < n; ++i) {
+        rb[i].reset(new netflow::PacketBuffer(kHeadroom + 1536, kHeadroom, desc[i].len));
+        rp[i].reset(new netflow::Packet(rb[i].get()));
+        ptrs[i] = rp[i].get();
+    }
+    auto restore_ref = [&] {
+        parallel(threads, [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i)
+                std::memcpy(rb[i]->get_data_start_ptr(), pristine.data() + (size_t)desc[i].off16 * 16, desc[i].len);
+        });
+    };
+    auto ref_data = [&](size_t i) -> const uint8_t* { return rb[i]->get_data_start_ptr(); };
+    auto time_reps = [&](const std::function<void()>& restore, const std::function<int()>& call, Timing& t) -> int {
+        restore();
+        int r = call();  // warm: staging ring, pinned buffers, code
+        for (size_t k = 0; k < reps && r == NFCS_OK; ++k) {
+            restore();
+            const auto t0 = clk::now();
+            r = call();
+            t.s.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+        }
+        return r;
+    };
+
+    Timing gpu, pool, ref1, refn;
+    rc = time_reps(restore_ref, [&] { return netflow_amd::update_checksums_batch(ptrs.data(), n); }, gpu);
+    if (rc) { std::printf("{\"error\": \"update_checksums_batch: %s\"}\n", nfcs_strerror(rc)); return 1; }
+    gpu.digest = digest(ref_data);
+
+    time_reps(restore_ref, [&] { for (size_t i = 0; i < n; ++i) ptrs[i]->update_checksums(); return 0; }, ref1);
+    ref1.digest = digest(ref_data);
+    time_reps(restore_ref, [&] {
+        parallel(threads, [&](size_t i0, size_t i1) { for (size_t i = i0; i < i1; ++i) ptrs[i]->update_checksums(); });
+        return 0;
+    }, refn);
+    refn.digest = digest(ref_data);
+    rb.clear();  // the reference's buffers are done with
+    rp.clear();
+
+    // the same frames in BufferPool slots (one pinned arena, 2176-byte slots, 32 bytes of headroom)
+    {
+        netflow_amd::BufferPool bp(n, 2176, *eng);
+        std::vector<netflow_amd::PacketBuffer*> pb(n);
+        std::vector<std::unique_ptr<netflow_amd::Packet>> pp(n);
+        std::vector<netflow_amd::Packet*> pptr(n);
+        for (size_t i = 0; i < n; ++i) {
+            pb[i] = bp.allocate_buffer(desc[i].len);
+            pb[i]->set_data_len(desc[i].len);
+            pp[i].reset(new netflow_amd::Packet(pb[i]));
+            pptr[i] = pp[i].get();
+        }
+        auto restore_pool = [&] {
+            parallel(threads, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i)
+                    std::memcpy(pb[i]->get_data_start_ptr(), pristine.data() + (size_t)desc[i].off16 * 16, desc[i].len);
+            });
+        };
+        rc = time_reps(restore_pool, [&] { return bp.update_checksums_batch(pptr.data(), n); }, pool);
+        if (rc) { std::printf("{\"error\": \"BufferPool::update_checksums_batch: %s\"}\n", nfcs_strerror(rc)); return 1; }
+        pool.digest = digest([&](size_t i) -> const uint8_t* { return pb[i]->get_data_start_ptr(); });
+        pp.clear();
+        for (auto* b : pb) bp.free_buffer(b);
+    }
+    nfcs_device_free(c, d_arena);
+    nfcs_device_free(c, d_desc);
+    std::printf("{\"packets\": %zu, \"frame_bytes\": %.0f, \"reps\": %zu, \"threads\": %zu, \"reference_digest\": \"%s\", "
+                "\"adapter\": %s, \"buffer_pool\": %s, \"reference_1_thread\": %s, \"reference_threads\": %s}\n",
+                n, frame_bytes, reps, threads, want.c_str(), stats(gpu).c_str(), stats(pool).c_str(), stats(ref1).c_str(),
+                stats(refn).c_str());
+    return gpu.digest == want && pool.digest == want && ref1.digest == want && refn.digest == want ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (mode == "adapterbench")
+        return adapterbench_mode(argc > 2 ? std::stoul(argv[2]) : (1u << 20), argc > 3 ? std::stoul(argv[3]) : 3,
+                                 argc > 4 ? std::stoul(argv[4]) : 16, argc > 5 ? argv[5] : "");
     if (mode == "cpubench")
         return cpubench_mode(argc > 2 ? std::stoul(argv[2]) : 1500, argc > 3 ? std::stoul(argv[3]) : 4096,
                              argc > 4 ? std::stoul(argv[4]) : 50);

@@ -50,6 +50,7 @@ def test_error_conventions_without_gpu(lib):
     # null context / arguments are rejected, never crash
     assert lib.nfcs_update_device(None, None, 0, None, 0, None, None, None) == -1
     assert lib.nfcs_update_host(None, None, 0, None, 0, None, 0) == -1
+    assert lib.nfcs_update_host_frames(None, None, None, 0, None, 0) == -1
     assert lib.nfcs_ctx_create(0, None) == -1
     assert lib.nfcs_ctx_set_slot_bytes(None, 128) == -1
     c = ctypes.c_void_p()

@@ -59,13 +59,29 @@ def test_host_path_argument_rules(engine):
     L = nf.lib()
     arena, desc = oracle.pack_frames(_frames())
     n = len(desc)
-    rev = np.ascontiguousarray(desc[::-1])  # nfcs_update_host takes frames in arena order
     before = arena.copy()
-    assert L.nfcs_update_host(engine.ctx, arena.ctypes.data, arena.nbytes, rev.ctypes.data, n, None, 0) == EINVAL
     # zero-copy needs a pinned arena; this one is pageable
     assert L.nfcs_update_host(engine.ctx, arena.ctypes.data, arena.nbytes, desc.ctypes.data, n, None,
                               nf.HOST_ZERO_COPY) == EINVAL
     assert np.array_equal(arena, before)
+    # scattered frames: a NULL pointer array with n > 0, and a non-zero (reserved) flags word
+    lens = np.ascontiguousarray(desc["len"])
+    assert L.nfcs_update_host_frames(engine.ctx, None, lens.ctypes.data, n, None, 0) == EINVAL
+    ptrs = (arena.ctypes.data + desc["off16"].astype(np.uint64) * 16).astype(np.uint64)
+    assert L.nfcs_update_host_frames(engine.ctx, ptrs.ctypes.data, lens.ctypes.data, n, None, 1) == EINVAL
+    assert np.array_equal(arena, before)
+
+
+def test_host_path_takes_descriptors_in_any_order(engine):
+    """Round 5: nfcs_update_host no longer requires arena order — descriptors
+    in reverse order (every frame its own run of ascending offsets) give the oracle's bytes and
+    statuses, per descriptor."""
+    arena, desc = oracle.pack_frames(_frames())
+    rev = np.ascontiguousarray(desc[::-1])
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, rev)
+    st = engine.update_host(arena, rev)
+    assert np.array_equal(st, rst) and np.array_equal(arena, ref)
 
 
 def test_descriptor_outside_the_arena_is_a_status_not_an_error(engine):

@@ -155,3 +155,56 @@ def test_update_waves_spanning_32_gib(engine, big, slot):
         engine.set_slot_bytes(0)
         d_desc.free()
         d_st.free()
+
+
+@pytest.mark.parametrize("delta16", [(1 << 28) - (1 << 13) - 1, (1 << 28) - (1 << 13)])
+def test_update_waves_at_the_wave_buffer_span_boundary(engine, big, delta16):
+    """The short shape's per-wave buffer resource (nfcs_kernels.hip wave_buf): a wave whose
+    rows' frames span delta16 16-byte units — kBufSpan16 - 1 (the last span the buffer path takes,
+    offsets up to 4 GiB - 128 KiB into the wave's buffer) and kBufSpan16 (the first the global-load
+    path takes). Rows 0-2 of every wave lie in one region, row 3 exactly delta16 units above row 0, so
+    every wave's span is exactly delta16. An off-by-one in the span check or the out-of-range offset
+    would not fault: the lanes would read zeros and the checksums would differ from the oracle's."""
+    waves = 5000
+    n = 4 * waves
+    frames = [f[:1500] if len(f) > 1500 else f for f in oracle.fuzz_frames(55, 0, n)]
+    lo = 4096
+    off = np.zeros(n, np.uint64)
+    for w in range(waves):
+        a = lo + w * 3 * 1536
+        off[4 * w: 4 * w + 3] = [a, a + 1536, a + 3072]
+        off[4 * w + 3] = a + delta16 * 16
+    assert int(off.max()) + 1536 < BASE
+    packed, pdesc = oracle.pack_frames(frames)
+    ref = packed.copy()
+    rst, _ = oracle.update_batch(ref, pdesc, nthreads=8)
+    region_a = np.zeros(waves * 3 * 1536, np.uint8)
+    region_b = np.zeros(waves * 3 * 1536 + 1536, np.uint8)
+    b0 = lo + delta16 * 16
+    for i, f in enumerate(frames):
+        o = int(off[i])
+        dst, base = (region_a, lo) if i % 4 != 3 else (region_b, b0)
+        dst[o - base: o - base + len(f)] = np.frombuffer(f, np.uint8)
+    big.upload(region_a, lo)
+    big.upload(region_b, b0)
+    desc = np.zeros(n, dtype=nf.DESC_DTYPE)
+    desc["off16"] = (off // 16).astype(np.uint32)
+    desc["len"] = [len(f) for f in frames]
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_st = engine.alloc(n)
+    try:
+        engine.set_slot_bytes(900)  # the short shape (16-lane rows, one-wave workgroups, buffer loads)
+        engine.update_device(big, b0 + region_b.nbytes, d_desc, n, d_st)
+        engine.sync()
+        assert np.array_equal(d_st.download(np.uint8, n), rst)
+        got_a = big.download(np.uint8, region_a.nbytes, lo)
+        got_b = big.download(np.uint8, region_b.nbytes, b0)
+        for i, f in enumerate(frames):
+            o = int(off[i])
+            g, base = (got_a, lo) if i % 4 != 3 else (got_b, b0)
+            p = int(pdesc[i]["off16"]) * 16
+            assert np.array_equal(g[o - base: o - base + len(f)], ref[p: p + len(f)]), i
+    finally:
+        engine.set_slot_bytes(0)
+        d_desc.free()
+        d_st.free()

@@ -162,3 +162,79 @@ def test_ring_burst_adapts_without_hint(engine):
         engine.set_slot_bytes(0)
         a.free()
         d.free()
+
+
+def test_footprint_sampled_over_the_whole_sub_batched_call(engine):
+    """A 1M-packet burst in a ring of 2176-byte slots whose first 512K frames are 1500 bytes long and
+    whose last 512K are 64 bytes (arena_bytes / n = 2176 says long, so the call runs as two 512K
+    sub-batches and samples): the footprint read back reflects BOTH halves, (1536 + 128) / 2 = 832
+    bytes, not the first sub-batch's 1536 (round 5: the first sub-batch samples 256 descriptors
+    spread over the whole call). Bytes equal the oracle's."""
+    n, slot = 1 << 20, 2176
+    h1, d1 = ring_burst(n // 2, 1500, slot, 21)
+    h2, d2 = ring_burst(n // 2, 64, slot, 22)
+    host = np.concatenate([h1, h2])
+    desc = np.concatenate([d1, d2])
+    desc["off16"][n // 2:] += (n // 2) * (slot // 16)
+    ring = host.nbytes
+    ref = host.copy()
+    oracle.update_batch(ref, desc, nthreads=8)
+    engine.set_slot_bytes(0)
+    a = engine.alloc(ring).upload(host)
+    d = engine.alloc(desc.nbytes).upload(desc)
+    try:
+        assert engine.launch_footprint(ring, d, n) == slot
+        engine.update_device(a, ring, d, n)
+        engine.sync()
+        assert np.array_equal(a.download(np.uint8, ring), ref)
+        fp = engine.launch_footprint(ring, d, n)
+        assert 700 <= fp <= 960, fp
+        engine.update_device(a, ring, d, n)  # now the short shape: same bytes (idempotent)
+        engine.sync()
+        assert np.array_equal(a.download(np.uint8, ring), ref)
+    finally:
+        a.free()
+        d.free()
+
+
+def test_footprint_kept_per_burst_across_a_rotation(engine):
+    """Calls rotating over three bursts (descriptor arrays) of 64-byte frames in 4 KiB-slot rings, no
+    hint: each burst keeps its own sample (8 observation slots per context, least recently used
+    replaced), so every one adapts after its first call — round 4 kept one, and a rotation never
+    adapted. A sample of a replaced burst's generation is never taken for another's."""
+    n, L, slot = 1 << 16, 64, 4096
+    bursts = []
+    engine.set_slot_bytes(0)
+    try:
+        for k in range(3):
+            host, desc = ring_burst(n, L, slot, 30 + k)
+            ref = host.copy()
+            oracle.update_batch(ref, desc, nthreads=8)
+            bursts.append((engine.alloc(host.nbytes).upload(host), engine.alloc(desc.nbytes).upload(desc), ref))
+        for rnd in range(2):
+            for a, d, ref in bursts:
+                engine.update_device(a, ref.nbytes, d, n)
+                engine.sync()
+                assert np.array_equal(a.download(np.uint8, ref.nbytes), ref)
+        for a, d, ref in bursts:
+            fp = engine.launch_footprint(ref.nbytes, d, n)
+            assert 128 <= fp < 800, fp  # each burst's own sample: 64-byte frames round up to 128
+        # 8 more bursts push the first three out: their footprint is arena_bytes / n again
+        others = [engine.alloc(16 * n) for _ in range(8)]
+        try:
+            for k, o in enumerate(others):
+                od = np.zeros(n, dtype=oracle.DESC_DTYPE)
+                od["off16"] = np.arange(n, dtype=np.uint32) * (slot // 16)
+                od["len"] = L
+                o.upload(od)
+                engine.update_device(bursts[k % 3][0], bursts[k % 3][2].nbytes, o, n)
+            engine.sync()
+            for a, d, ref in bursts:
+                assert engine.launch_footprint(ref.nbytes, d, n) == ref.nbytes // n
+        finally:
+            for o in others:
+                o.free()
+    finally:
+        for a, d, _ in bursts:
+            a.free()
+            d.free()

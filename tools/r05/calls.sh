@@ -1,0 +1,34 @@
+#!/bin/bash
+# The round-5 GPU calls, one function per call (the exact command each ran through gpurun, from the repo
+# root): `bash tools/r05/calls.sh <letter>`. Their results are in profiles/r05_*; the libraries they name
+# are built here by tools/r05/build_lib.sh (git-ignored).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+
+# one bench line per library, alternating libraries within each round, on one box
+ab_lines() {  # ab_lines OUTDIR ROUNDS "LIBS" "NAME ARGS" ...
+  local out=$1 rounds=$2 libs=$3; shift 3
+  for r in $(seq 1 "$rounds"); do for lib in $libs; do
+    for spec in "$@"; do
+      set -- $spec; local name=$1; shift
+      NFCS_LIB=tools/r05/lib$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay --no-mix \
+        > "$out/${name}_${lib}_$r.json" 2>> "$out/bench.err" || return 1
+    done
+  done; done
+}
+
+call_a() {
+  # round 5, GPU call a: the GPU tests on the product with per-slot zero lines (g_zero_pool), ring-wrapping
+  # host bursts, scattered host frames (nfcs_update_host_frames) and tagged footprint samples; the new
+  # default bench line (c3 / l3fwd_c3 / host_adapter sub-lines), then the zero-target A/B: round 4's
+  # product (one 16-byte g_zero16),
+  # per-slot lines at 128 B / 256 B / 4 KB strides, the 128-B form in three libraries whose data sections
+  # differ (pads of 0 / 1536 / 2304 bytes move the pool by a page), and one aligned shared chunk
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5a && \
+  timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5a/pytest.log 2>&1 && \
+  timeout -k 10 300 python3 -u bench.py > gpurun_out/r5a/bench.json 2> gpurun_out/r5a/bench.err && \
+  ab_lines gpurun_out/r5a 3 "nfcs_r4final z_s8 z_s8_p1536 z_s8_p2304 z_s16 z_s256 z_single" \
+    "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40"
+}
+
+"call_$1"
