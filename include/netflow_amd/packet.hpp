@@ -608,26 +608,33 @@ inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uin
                                               uint32_t flags) {
     if (n == 0) return NFCS_OK;
     if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
-    std::vector<std::pair<uint32_t, uint32_t>> order(n);  // (off16, packet index)
     std::vector<nfcs_desc> desc(n);
+    size_t drops = 0;  // places where the burst's arena offsets go down (a wrap of the pool's slots)
     for (size_t i = 0; i < n; ++i) {
         PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
         const unsigned char* d = b ? b->get_data_start_ptr() : nullptr;
         if (!b || !in_arena(b) || ((d - arena_) & 15))
             return eng_.update_checksums_batch(pkts, n, status);
-        order[i] = {static_cast<uint32_t>((d - arena_) >> 4), static_cast<uint32_t>(i)};
+        desc[i] = nfcs_desc{static_cast<uint32_t>((d - arena_) >> 4), static_cast<uint32_t>(b->get_data_length())};
+        drops += i && desc[i].off16 < desc[i - 1].off16;
     }
-    std::sort(order.begin(), order.end());  // nfcs_update_host takes frames in arena order
-    for (size_t j = 0; j < n; ++j) {
-        PacketBuffer* b = pkts[order[j].second]->get_buffer();
-        desc[j] = nfcs_desc{order[j].first, static_cast<uint32_t>(b->get_data_length())};
+    // nfcs_update_host stages each run of ascending offsets as one span: a burst in allocation order
+    // (the pool hands slots out in arena order) or wrapping once goes as it is; a burst in an order
+    // the pool's reuse has scrambled is sorted first, so its spans stay long
+    if (drops <= 1) {
+        return eng_.update_host(arena_, slots_ * slot_bytes_, desc.data(), static_cast<uint32_t>(n), status, flags);
     }
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = static_cast<uint32_t>(i);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return desc[a].off16 < desc[b].off16; });
+    std::vector<nfcs_desc> sorted(n);
+    for (size_t j = 0; j < n; ++j) sorted[j] = desc[order[j]];
     std::vector<uint8_t> st(status ? n : 0);
-    const int rc = eng_.update_host(arena_, slots_ * slot_bytes_, desc.data(), static_cast<uint32_t>(n),
+    const int rc = eng_.update_host(arena_, slots_ * slot_bytes_, sorted.data(), static_cast<uint32_t>(n),
                                     status ? st.data() : nullptr, flags);
     if (rc) return rc;
     if (status)
-        for (size_t j = 0; j < n; ++j) status[order[j].second] = st[j];
+        for (size_t j = 0; j < n; ++j) status[order[j]] = st[j];
     return NFCS_OK;
 }
 

@@ -31,7 +31,7 @@ enum : int {
 
 // In the long shape (mean footprint >= kSmallMeanBytes) a wave whose four frames average at least
 // this many bytes defers its checksum stores to the write pass (kUpdateAuto); the short and tiny
-// shapes store every wave inline (round 3: no write pass for them, launch_update_one). Uniform-length sweeps (tools/exp/len_sweep.sh, 1M frames, DESIGN.md
+// shapes store every wave inline (round 3: no write pass for them, launch_update_one). Uniform-length sweeps (round 2, tools/exp/len_sweep.sh in git b164560^; 1M frames, DESIGN.md
 // §5e): at 1024 B inline stores win (0.661 vs 0.635), at 1280 B deferral wins (replayed 0.782 vs
 // 0.768, fresh 0.760 vs 0.624), at 1500 B too (0.759 / 0.745 vs 0.757 / 0.653). Short frames' reads
 // are latency-bound and hide the inline stores; a mixed batch like C3 (U{64..1500}) lost 3.5% when
@@ -39,7 +39,7 @@ enum : int {
 constexpr uint32_t kDeferMeanBytes = 1280;
 // kUpdateAuto on a burst of at most this many packets stores every wave inline from one kernel:
 // the write pass's launch (~3 µs) outweighs what deferral saves on so few packets (burst sweep,
-// tools/exp/ab.py c<k>n<N>, DESIGN.md §5e: 1K-64K C1 packets 13-35% faster, 64K C3 16%; 64K C2
+// round 2, tools/exp/ab.py c<k>n<N> in git b164560^; DESIGN.md §5e: 1K-64K C1 packets 13-35% faster, 64K C3 16%; 64K C2
 // jumbo frames 5% slower; 128K C1 even). The packet count alone decides: the arena size never
 // changes the form.
 constexpr uint32_t kInlineMaxPackets = 65536;

@@ -25,6 +25,8 @@
 //   icmp-gpu / icmp-cpu  (no input) IcmpProcessorTest's scenarios (tests/icmp_processor_test.cpp:
 //         278-407) and the packets IcmpProcessor builds from them (icmp_processor.cpp:96-180,
 //         255-336), in two stages of update_checksums() over bursts (see icmp_mode).
+//   adapterbench [n reps threads want]  the reference's call convention end to end, timed (bench.py's
+//         host_adapter sub-line; see adapterbench_mode). Prints one JSON line.
 // Frames where the reference itself reads or writes outside its buffer (IHL past the frame; a push
 // without tailroom into a buffer whose capacity holds len + 4; a re-tag of a runt in a buffer of
 // fewer than 16 bytes) are skipped: there the reference is undefined.
@@ -679,7 +681,7 @@ int adapterbench_mode(size_t n, size_t reps, size_t threads, const std::string& 
         return r;
     };
 
-    Timing gpu, pool, ref1, refn;
+    Timing gpu, pool, pool_zc, pool_gather, ref1, refn;
     rc = time_reps(restore_ref, [&] { return netflow_amd::update_checksums_batch(ptrs.data(), n); }, gpu);
     if (rc) { std::printf("{\"error\": \"update_checksums_batch: %s\"}\n", nfcs_strerror(rc)); return 1; }
     gpu.digest = digest(ref_data);
@@ -712,19 +714,39 @@ int adapterbench_mode(size_t n, size_t reps, size_t threads, const std::string& 
                     std::memcpy(pb[i]->get_data_start_ptr(), pristine.data() + (size_t)desc[i].off16 * 16, desc[i].len);
             });
         };
+        auto pool_data = [&](size_t i) -> const uint8_t* { return pb[i]->get_data_start_ptr(); };
         rc = time_reps(restore_pool, [&] { return bp.update_checksums_batch(pptr.data(), n); }, pool);
         if (rc) { std::printf("{\"error\": \"BufferPool::update_checksums_batch: %s\"}\n", nfcs_strerror(rc)); return 1; }
-        pool.digest = digest([&](size_t i) -> const uint8_t* { return pb[i]->get_data_start_ptr(); });
+        pool.digest = digest(pool_data);
+        // the same pool buffers read by the kernel over PCIe in place (NFCS_HOST_ZERO_COPY), and
+        // gathered by nfcs_update_host_frames (frame bytes only over PCIe, not the slots' gaps)
+        rc = time_reps(restore_pool, [&] { return bp.update_checksums_batch(pptr.data(), n, nullptr, NFCS_HOST_ZERO_COPY); },
+                       pool_zc);
+        if (rc) { std::printf("{\"error\": \"zero-copy: %s\"}\n", nfcs_strerror(rc)); return 1; }
+        pool_zc.digest = digest(pool_data);
+        std::vector<uint8_t*> fp(n);
+        std::vector<uint32_t> fl(n);
+        for (size_t i = 0; i < n; ++i) {
+            fp[i] = pb[i]->get_data_start_ptr();
+            fl[i] = (uint32_t)desc[i].len;
+        }
+        rc = time_reps(restore_pool, [&] { return nfcs_update_host_frames(c, fp.data(), fl.data(), (uint32_t)n, nullptr, 0); },
+                       pool_gather);
+        if (rc) { std::printf("{\"error\": \"gather: %s\"}\n", nfcs_strerror(rc)); return 1; }
+        pool_gather.digest = digest(pool_data);
         pp.clear();
         for (auto* b : pb) bp.free_buffer(b);
     }
     nfcs_device_free(c, d_arena);
     nfcs_device_free(c, d_desc);
     std::printf("{\"packets\": %zu, \"frame_bytes\": %.0f, \"reps\": %zu, \"threads\": %zu, \"reference_digest\": \"%s\", "
-                "\"adapter\": %s, \"buffer_pool\": %s, \"reference_1_thread\": %s, \"reference_threads\": %s}\n",
-                n, frame_bytes, reps, threads, want.c_str(), stats(gpu).c_str(), stats(pool).c_str(), stats(ref1).c_str(),
-                stats(refn).c_str());
-    return gpu.digest == want && pool.digest == want && ref1.digest == want && refn.digest == want ? 0 : 1;
+                "\"adapter\": %s, \"buffer_pool\": %s, \"buffer_pool_zero_copy\": %s, \"buffer_pool_gather\": %s, "
+                "\"reference_1_thread\": %s, \"reference_threads\": %s}\n",
+                n, frame_bytes, reps, threads, want.c_str(), stats(gpu).c_str(), stats(pool).c_str(),
+                stats(pool_zc).c_str(), stats(pool_gather).c_str(), stats(ref1).c_str(), stats(refn).c_str());
+    for (const Timing* t : {&gpu, &pool, &pool_zc, &pool_gather, &ref1, &refn})
+        if (t->digest != want) return 1;
+    return 0;
 }
 
 }  // namespace

@@ -192,8 +192,9 @@ def test_timing_entries_with_no_packets(engine):
 
 
 def test_rotating_timing_matches_the_reference(engine):
-    """nfcs_time_update_batches (bench.py's `fresh` sub-line): rotating over 3 batches of fuzz frames,
-    every batch ends equal to the oracle's update of it."""
+    """nfcs_time_update_batches (the timing of bench.py's headline line and of its c4_shard / c3
+    sub-lines): rotating over 3 batches of fuzz frames, every batch ends equal to the oracle's update
+    of it."""
     bs, refs = [], []
     for k in range(3):
         arena, desc = oracle.pack_frames(oracle.fuzz_frames(600 + k, 0, 3000))

@@ -160,3 +160,23 @@ def test_single_packet_cpu_path_speed(exe):
     kv = dict(x.split("=") for x in r.stdout.split())
     assert int(kv["mismatches"]) == 0
     assert float(kv["speedup"]) > 1.5, r.stdout
+
+
+@pytest.mark.gpu
+def test_reference_call_convention_end_to_end(exe):
+    """bench.py's host_adapter sub-line at a test size: 65,536 C1 frames, each in its own
+    netflow::PacketBuffer (the reference's class, one `new[]` each), as one burst of netflow::Packet*
+    through netflow_amd::update_checksums_batch (nfcs_update_host_frames); the same frames in
+    netflow_amd::BufferPool slots (staged spans, zero-copy and gathered); and the reference's own
+    per-packet Packet::update_checksums() on 1 and 4 threads — every result's digest equal to the
+    oracle's digest of the updated batch (the oracle pinned to the reference, test_oracle.py)."""
+    n = 65536
+    _, dout, _ = oracle.config_digest(1, 20250620, 0, n)
+    want = f"{dout:016x}"
+    r = subprocess.run([exe, "adapterbench", str(n), "1", "4", want], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("adapter", "buffer_pool", "buffer_pool_zero_copy", "buffer_pool_gather", "reference_1_thread",
+              "reference_threads"):
+        assert out[k]["match"] and out[k]["digest"] == want, (k, out[k])
+    print({k: out[k]["GBps"] for k in out if isinstance(out[k], dict)})

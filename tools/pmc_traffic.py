@@ -30,9 +30,24 @@ KERNEL = {"update": ("update_rows_kernel", "apply_bytes_kernel"), "l3fwd": ("upd
           "vlan": ("vlan_rows_kernel",), "flowkey": ("flow_keys_lanes_kernel",)}
 
 
+def threads_per_packet(kernel_name: str) -> int:
+    """Work items per packet of a dispatch of one of the op's kernels, from its template arguments:
+    update_rows_kernel<K, R, ...> and vlan_rows_kernel<K, K2, POL, R, ...> run an R-lane row per
+    packet; the write passes and the flow-key kernel one lane per packet."""
+    if "update_rows_kernel<" in kernel_name:
+        return int(kernel_name.split("update_rows_kernel<", 1)[1].split(",")[1])
+    if "vlan_rows_kernel<" in kernel_name:
+        return int(kernel_name.split("vlan_rows_kernel<", 1)[1].split(",")[3])
+    return 1
+
+
 def run_pass(out, cfg, counters, steps, op="update", packets=0, align=128):
-    """One rocprofv3 pass with the given counters; per counter, the sum over the op's kernels of
-    the median over that kernel's launches."""
+    """One rocprofv3 pass with the given counters; per counter, the sum over the op's kernels of the
+    median over that kernel's dispatches of the counter per packet the dispatch covers (its grid size
+    / work items per packet), times the call's packets. A call that runs as several sub-batches
+    (nfcs_update_device above 512K long frames, the forward's deferred bursts) is so counted whole
+    from the dispatches the trace holds, whatever the thresholds (the number of sub-batches
+    is no longer predicted here)."""
     d = os.path.join(out, f"c{cfg}{'_' + str(packets) if packets else ''}_a{align}_{op}_{counters[0]}")
     cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d,
            "-o", "p", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(cfg),
@@ -41,18 +56,25 @@ def run_pass(out, cfg, counters, steps, op="update", packets=0, align=128):
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 failed ({r.returncode}): {r.stderr[-2000:]}")
+    n = packets or PACKETS[cfg]
     vals = {(k, c): [] for k in KERNEL[op] for c in counters}
+    covered = {k: 0.0 for k in KERNEL[op]}
     for root, _, files in os.walk(d):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for row in csv.DictReader(open(os.path.join(root, f))):
                     for k in KERNEL[op]:
                         if k in row["Kernel_Name"] and (k, row["Counter_Name"]) in vals:
-                            vals[(k, row["Counter_Name"])].append(float(row["Counter_Value"]))
+                            pk = int(row["Grid_Size"]) / threads_per_packet(row["Kernel_Name"])
+                            vals[(k, row["Counter_Name"])].append(float(row["Counter_Value"]) / pk)
+                            if row["Counter_Name"] == counters[0]:
+                                covered[k] += pk
     if not vals[(KERNEL[op][0], counters[0])]:
         raise SystemExit(f"no {counters[0]} samples for {KERNEL[op][0]} in {d}")
-    med = {c: sum(statistics.median(vals[(k, c)]) for k in KERNEL[op] if vals[(k, c)]) for c in counters}
-    return med, len(vals[(KERNEL[op][0], counters[0])])
+    med = {c: sum(statistics.median(vals[(k, c)]) * n for k in KERNEL[op] if vals[(k, c)]) for c in counters}
+    # launches per call: the read-pass dispatches over the packets they covered, per n packets
+    per_call = len(vals[(KERNEL[op][0], counters[0])]) * n / covered[KERNEL[op][0]]
+    return med, len(vals[(KERNEL[op][0], counters[0])]), per_call
 
 
 def main():
@@ -77,30 +99,19 @@ def main():
         res = json.load(open(a.merge))
     for cfg, op in [(c, o) for o in a.ops for c in a.configs]:
         P = a.packets
-        f, nf_ = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op, P, a.align)
-        w, nw = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op, P, a.align)
-        q, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
-                        a.steps, op, P, a.align)
-        wq, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P, a.align)
+        f, nf_, sub = run_pass(a.out, cfg, ["FETCH_SIZE"], a.steps, op, P, a.align)
+        w, nw, _ = run_pass(a.out, cfg, ["WRITE_SIZE"], a.steps, op, P, a.align)
+        q, _, _ = run_pass(a.out, cfg, ["TCC_BUBBLE_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"],
+                           a.steps, op, P, a.align)
+        wq, _, _ = run_pass(a.out, cfg, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"], a.steps, op, P, a.align)
         key = ("C4_shard" if (cfg == 1 and P == 1 << 22) else f"C{cfg}" + (f"_{P}" if P else "")) + \
             ("" if op == "update" else f"_{op}") + ("" if a.align == 128 else f"_align{a.align}")
-        # launches per call: nfcs_update_device runs a long-frame batch of more than 512K packets
-        # (kSubBatchAbovePackets; 1M before round 4 session 2) as 512K-packet sub-batches (kSubBatchPackets), each its own read
-        # pass + write pass; the fused forward does so for long-frame bursts of more than 64K
-        # (kFwdDeferAbovePackets, round 4): C1 = 2 sub-batches. Mixes (C3) run one kernel.
-        n_ = P or PACKETS[cfg]
-        above = {"update": 1 << 19, "l3fwd": 1 << 16}.get(op)
-        sub = -(-n_ // (1 << 19)) if (above and cfg in (1, 2) and n_ > above) else 1
-        f = {k: v * sub for k, v in f.items()}
-        w = {k: v * sub for k, v in w.items()}
-        q = {k: v * sub for k, v in q.items()}
-        wq = {k: v * sub for k, v in wq.items()}
         fb, wb = 2 * f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
         rq = q["TCC_EA0_RDREQ_sum"]
         rb_req = rq * 128
         res[key] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                           "per_packet": (fb + wb) / (P or PACKETS[cfg]), "launches": min(nf_, nw),
-                    "launches_per_call": sub,
+                    "launches_per_call": round(sub, 3),
                           "read_bytes_from_requests": rb_req, "read_requests": rq,
                           "write_requests": wq["TCC_EA0_WRREQ_sum"],
                           "write_requests_64B": wq["TCC_EA0_WRREQ_64B_sum"]}

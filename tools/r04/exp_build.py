@@ -12,6 +12,7 @@ import sys
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+REV = "00f5686"  # the round-4 final tree
 ROOT = os.path.dirname(os.path.dirname(HERE))
 
 
@@ -25,9 +26,11 @@ def main():
         exp, args = os.path.abspath(args[1]), args[2:]
     if len(args) % 2:
         raise SystemExit(__doc__)
-    csrc = os.path.join(ROOT, "netflow_amd", "csrc")
     names = ("nfcs_kernels.hip", "nfcs_api.hip", "nfcs_internal.h")
-    srcs = {f: open(os.path.join(csrc, f)).read() for f in names}
+    # fresh_exp.hip instantiates round 4's row_stage / row_process (its COLD and KC knobs, dropped from
+    # the product in round 5): the product sources as of the round-4 final tree, from git
+    srcs = {f: subprocess.run(["git", "-C", ROOT, "show", f"{REV}:netflow_amd/csrc/{f}"], check=True,
+                              capture_output=True, text=True).stdout for f in names}
     for old, new in zip(args[::2], args[1::2]):
         cnt = 1
         if "*" in old[:4] and old.split("*", 1)[0].isdigit():

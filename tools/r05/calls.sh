@@ -23,12 +23,14 @@ call_a() {
   # default bench line (c3 / l3fwd_c3 / host_adapter sub-lines), then the zero-target A/B: round 4's
   # product (one 16-byte g_zero16),
   # per-slot lines at 128 B / 256 B / 4 KB strides, the 128-B form in three libraries whose data sections
-  # differ (pads of 0 / 1536 / 2304 bytes move the pool by a page), and one aligned shared chunk
+  # differ (pads of 0 / 1536 / 2304 bytes move the pool by a page), and one aligned shared chunk; then
+  # C3's write schedules of tools/r05/c3_exp.hip (write workgroups of sub-batch j-1 inside j's read pass)
   cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5a && \
   timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5a/pytest.log 2>&1 && \
   timeout -k 10 300 python3 -u bench.py > gpurun_out/r5a/bench.json 2> gpurun_out/r5a/bench.err && \
   ab_lines gpurun_out/r5a 3 "nfcs_r4final z_s8 z_s8_p1536 z_s8_p2304 z_s16 z_s256 z_single" \
-    "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40"
+    "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40" && \
+  timeout -k 10 200 python3 -u tools/r05/c3_forms.py --variants 0,1,2,3,4,5 --rounds 3 > gpurun_out/r5a/c3_forms.jsonl 2>&1
 }
 
 "call_$1"
