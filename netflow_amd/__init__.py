@@ -315,7 +315,7 @@ class Engine:
         offsets = np.asarray(offsets, dtype=np.int64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         n = len(lens)
-        assert len(offsets) == n and (n == 0 or int(offsets.max()) + int(lens.max()) <= buf.nbytes)
+        assert len(offsets) == n and (n == 0 or int((offsets + lens.astype(np.int64)).max()) <= buf.nbytes)
         ptrs = np.where(offsets < 0, 0, np.uint64(buf.ctypes.data) + offsets.astype(np.uint64)).astype(np.uint64)
         status = np.zeros(n, dtype=np.uint8) if want_status else None
         _check(lib().nfcs_update_host_frames(self.ctx, ptrs.ctypes.data if n else None,

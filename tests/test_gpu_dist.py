@@ -53,9 +53,10 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     """The N = 1 line (C1, BASELINE configs[1]) times the steady state — calls rotating over 4 separately
     generated batches, every batch's digest the reference's — and carries the one-batch replay
     sub-line, the C4-shard sub-line (the per-GPU batch the N > 1 lines scale, with its own roofline
-    fraction and the reference's digest of that shard), the host-memory (PCIe-inclusive) sub-line
-    from pinned and pageable arenas with the reference's digest, and the CPU baseline at the fastest
-    thread count measured."""
+    fraction and the reference's digest of that shard), the C3 and forward-C3 sub-lines, the
+    host-memory (PCIe-inclusive) sub-lines — an arena from pinned and pageable memory, and one
+    netflow::PacketBuffer per frame — with the reference's digest, and the CPU baseline at the
+    fastest thread count measured."""
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8", "--warmup", "2",
@@ -73,6 +74,12 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     assert 0.3 < c4["frac"] < 1.0 and c4["value"] > 0
     h = d["host"]
     assert h["parity"]["match"] is True and h["pinned"]["GBps"] > 0 and h["pageable"]["GBps"] > 0
+    # round 5: BASELINE C3's mix through the update and the fused forward, under the same clock
+    for k in ("c3", "l3fwd_c3"):
+        assert d[k]["parity"]["match"] is True and 0.2 < d[k]["frac"] < 1.0, (k, d[k])
+    # and the reference's own call convention (one netflow::PacketBuffer per frame) end to end
+    ha = d["host_adapter"]
+    assert ha["rc"] == 0 and ha["parity"]["match"] is True and ha["adapter"]["GBps"] > 0, ha
     cb = d["cpu_baseline"]
     assert cb["value"] == max(x["value"] for x in cb["runs"]) and cb["value"] > 0
     assert max(x["threads"] for x in cb["runs"]) == cb["nproc"] == len(os.sched_getaffinity(0))
