@@ -693,8 +693,8 @@ int adapterbench_mode(size_t n, size_t reps, size_t threads, const std::string& 
         return 0;
     }, refn);
     refn.digest = digest(ref_data);
-    rb.clear();  // the reference's buffers are done with
-    rp.clear();
+    rp.clear();  // the reference's Packets release their buffers' references first (packet.hpp:352-356)
+    rb.clear();
 
     // the same frames in BufferPool slots (one pinned arena, 2176-byte slots, 32 bytes of headroom)
     {
