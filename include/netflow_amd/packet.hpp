@@ -316,13 +316,29 @@ int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* 
     // then the transfers, then one scatter, one after the other)
     frames_.resize(n);
     lens_.resize(n);
-    for (size_t i = 0; i < n; ++i) {
-        auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
-        const size_t len = b ? b->get_data_length() : 0;
-        if (len > 0xFFFFFFFFu) return NFCS_EINVAL;
-        frames_[i] = b ? b->get_data_start_ptr() : nullptr;
-        lens_[i] = static_cast<uint32_t>(len);
+    // two dependent loads per packet (Packet -> PacketBuffer): split over a few threads for big bursts
+    std::atomic<bool> too_long{false};
+    auto fill = [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+            const size_t len = b ? b->get_data_length() : 0;
+            if (len > 0xFFFFFFFFu) too_long.store(true, std::memory_order_relaxed);
+            frames_[i] = b ? b->get_data_start_ptr() : nullptr;
+            lens_[i] = static_cast<uint32_t>(len);
+        }
+    };
+    const size_t nt = n >= (size_t(1) << 16) ? 8 : 1;
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) {
+        try {
+            th.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+        } catch (...) {  // no thread to be had: that range here (never throw)
+            fill(n * t / nt, n * (t + 1) / nt);
+        }
     }
+    fill(0, n / nt);
+    for (auto& x : th) x.join();
+    if (too_long.load()) return NFCS_EINVAL;
     return nfcs_update_host_frames(ctx_, frames_.data(), lens_.data(), static_cast<uint32_t>(n), status, 0);
 }
 

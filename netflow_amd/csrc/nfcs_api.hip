@@ -371,7 +371,13 @@ int ensure_host_pipeline(nfcs_ctx* ctx) {
 }
 
 int build_host_pipeline(nfcs_ctx* ctx) {
+    // host threads for the staging copies, gathers and write-back: 8, or NFCS_HOST_THREADS (1-64) —
+    // a caller that shares the host's cores with other work, or has more to give, sets it
     ctx->copy_threads = 8;
+    if (const char* e = getenv("NFCS_HOST_THREADS")) {
+        const int t = atoi(e);
+        if (t >= 1 && t <= 64) ctx->copy_threads = t;
+    }
     ctx->stage_bytes = nfcs_ctx::kStageBytes;
     ctx->stage_pkts = (uint32_t)(ctx->stage_bytes / 64);
     // staging ring on the GPU's NUMA node, copy threads on its CPUs
@@ -937,7 +943,13 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         const int ng = bytes >= (8u << 20) ? parts : 1;
         c->workers.run(ng, [&](int t) {
             const uint32_t j0 = (uint32_t)((uint64_t)m * t / ng), j1 = (uint32_t)((uint64_t)m * (t + 1) / ng);
+            constexpr uint32_t kPf = 4;  // the first lines of the frame kPf ahead: its misses overlap this copy
             for (uint32_t j = j0; j < j1; ++j) {
+                if (j + kPf < j1 && frames[i + j + kPf]) {
+                    __builtin_prefetch(frames[i + j + kPf], 0, 0);
+                    __builtin_prefetch(frames[i + j + kPf] + 64, 0, 0);
+                    __builtin_prefetch(frames[i + j + kPf] + 128, 0, 0);
+                }
                 const uint64_t len = hd[j].len, o = (uint64_t)hd[j].off16 * 16u;
                 if (len) memcpy(dst + o, frames[i + j], len);
                 memset(dst + o + len, 0, pad(len) - len);  // the kernel reads whole 16-byte chunks

@@ -6,12 +6,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 
 # one bench line per library, alternating libraries within each round, on one box
-ab_lines() {  # ab_lines OUTDIR ROUNDS "LIBS" "NAME ARGS" ...
+ab_lines() {  # ab_lines OUTDIR ROUNDS "LIBS" "NAME ARGS" ... (LIB "cur" = the product library)
   local out=$1 rounds=$2 libs=$3; shift 3
+  local specs=("$@") r lib spec name path
   for r in $(seq 1 "$rounds"); do for lib in $libs; do
-    for spec in "$@"; do
-      set -- $spec; local name=$1; shift
-      NFCS_LIB=tools/r05/lib$lib.so timeout -k 10 200 python3 -u bench.py "$@" --no-cpu --no-host --no-c4 --no-replay --no-mix \
+    path=tools/r05/lib$lib.so; [ "$lib" = cur ] && path=netflow_amd/libnfcs.so
+    for spec in "${specs[@]}"; do
+      read -r name args <<< "$spec"
+      NFCS_LIB=$path timeout -k 10 200 python3 -u bench.py $args --no-cpu --no-host --no-c4 --no-replay --no-mix \
         > "$out/${name}_${lib}_$r.json" 2>> "$out/bench.err" || return 1
     done
   done; done
@@ -24,7 +26,9 @@ call_a() {
   # product (one 16-byte g_zero16),
   # per-slot lines at 128 B / 256 B / 4 KB strides, the 128-B form in three libraries whose data sections
   # differ (pads of 0 / 1536 / 2304 bytes move the pool by a page), and one aligned shared chunk; then
-  # C3's write schedules of tools/r05/c3_exp.hip (write workgroups of sub-batch j-1 inside j's read pass)
+  # C3's write schedules of tools/r05/c3_exp.hip (write workgroups of sub-batch j-1 inside j's read pass).
+  # (As it ran, ab_lines reset "$@" inside its loop: after the first library the A/B ran C1 lines under
+  # wrong names; call b repeats the A/B. The tests, the bench line and the C3 forms are as listed.)
   cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5a && \
   timeout -k 10 400 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5a/pytest.log 2>&1
   local rc=$?; [ $rc -le 1 ] || return $rc  # failed tests (1) still let the measurements run; nothing else does
@@ -32,6 +36,24 @@ call_a() {
   ab_lines gpurun_out/r5a 3 "nfcs_r4final z_s8 z_s8_p1536 z_s8_p2304 z_s16 z_s256 z_single" \
     "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40" && \
   timeout -k 10 200 python3 -u tools/r05/c3_forms.py --variants 0,1,2,3,4,5 --rounds 3 > gpurun_out/r5a/c3_forms.jsonl 2>&1
+}
+
+
+call_b() {
+  # round 5, GPU call b: call a's zero-target A/B again (its loop had a shell bug): round 4's product
+  # (one 16-byte g_zero16) against the product (per-slot zero lines), the product in two libraries whose
+  # data sections differ (pads of 1536 / 2304 bytes move the pool by a page), per-slot lines at a 4 KB
+  # stride and one page-aligned shared chunk; C1, C3 and the forward's C3 mix, alternating on one box.
+  # Then the host paths with 8 and 16 copy threads (NFCS_HOST_THREADS)
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5b && \
+  ab_lines gpurun_out/r5b 3 "nfcs_r4final cur cur_p1536 cur_p2304 z_s256 z_single" \
+    "c1 --steps 50" "c3 --config 3 --steps 40" "fwdc3 --op l3fwd --config 3 --steps 40" && \
+  for t in 8 16; do
+    NFCS_HOST_THREADS=$t timeout -k 10 200 tests/cpp/_ref/netflow_adapter_test adapterbench 1048576 3 16 81cc3905092d7f44 \
+      > gpurun_out/r5b/adapter_t$t.json 2> gpurun_out/r5b/adapter_t$t.err || exit 1
+    NFCS_HOST_THREADS=$t timeout -k 10 300 python3 -u bench.py --no-cpu --no-replay --no-mix --steps 10 \
+      > gpurun_out/r5b/bench_host_t$t.json 2>> gpurun_out/r5b/bench.err || exit 1
+  done
 }
 
 "call_$1"
