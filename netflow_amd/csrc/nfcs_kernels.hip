@@ -48,29 +48,10 @@ DEV uint32_t xcd_block_n(uint32_t nblocks) {
 DEV uint32_t xcd_block() { return xcd_block_n(gridDim.x); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// Targets of the loads of lanes past their frame (or, in a line-aligned window, before it): every
-// load is issued by every lane, so a wave's compiler-counted vmcnt waits stay static. Round 5: a
-// pool of kZeroLines zero 128-byte lines, aligned to 4 KB, and each WAVE aims all such lanes at one
-// chunk of its own line (zero_chunk): one request per load instruction, as with one shared chunk,
-// but the waves' requests spread over every L2 channel. Round 4 aimed every lane of the chip at one
-// 16-byte global; its channel took up to half the load requests of a short-frame batch, and the
-// fused forward's C3 mix moved between 0.68 and 0.75 ms per call with that global's link-time address
-// and from run to run (profiles/r04_s2_zero_target_ab.jsonl; round 5: profiles/r05_zero_pool_ab.jsonl).
-constexpr uint32_t kZeroLines = 512;
-#ifdef NFCS_DATA_PAD
-__device__ __attribute__((used)) uint8_t g_data_pad[NFCS_DATA_PAD];
-#endif
-__device__ __attribute__((aligned(4096))) uint4 g_zero_pool[kZeroLines * 8];
-#ifndef NFCS_ZMODE
-#define NFCS_ZMODE 2
-#endif
-#ifndef NFCS_ZSTRIDE
-#define NFCS_ZSTRIDE 8
-#endif
-DEV const uint4* zero_chunk(uint64_t wave) {
-    return (NFCS_ZMODE & 1) ? g_zero_pool + ((uint32_t)wave & (kZeroLines - 1u)) * 8u : g_zero_pool;
-}
-DEV const uint4* zslot(const uint4* zl, int k) { return (NFCS_ZMODE & 2) ? zl + ((k * NFCS_ZSTRIDE) & (kZeroLines * 8 - 1)) : zl; }
+// A zero line, 4 KB-aligned (its page offset never depends on what the linker puts before it): the
+// target of the loads past a frame where no frame line is at hand — VLAN, flow keys, continuation
+// batches of jumbo frames, the bench's stream reads, and instructions with no lane in its frame (past_addr).
+__device__ __attribute__((aligned(4096))) uint4 g_zero_line[8];
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
 DEV uint32_t comp(const uint4& v, uint32_t j) {
@@ -687,6 +668,39 @@ DEV WaveBuf wave_buf(const DescW<P>& D, uint64_t pw, uint32_t n, uint8_t* arena,
     return b;
 }
 
+// Where the row kernels' lanes past their frame load from (round 5). Every load is
+// issued by every lane, so the compiler's vmcnt waits stay counted, and a lane past its frame (or, in
+// a line-aligned window, before it) still needs an address. Round 4 aimed them all at one 16-byte
+// global: one extra request per load instruction, all of the chip's at one L2 channel per XCD, and the
+// fused forward's C3 mix moved between 0.68 and 0.75 ms per call with that global's link-time address
+// and from run to run. Now such a lane reads the chunk that the first in-frame lane of the SAME
+// instruction reads (ballot, find-first, two v_readlane): it adds no request at all; only an
+// instruction with no lane in its frame reads g_zero_line. Such lanes read another frame's bytes
+// instead of zeros: the sums never add them (they mask by region), and the header view the plan reads
+// is zeroed past the frame (row_process).
+typedef const __attribute__((address_space(1))) u32x4_t gu32x4;
+DEV uint64_t past_addr(uint64_t own, bool in) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+    const int first = m ? (int)__builtin_ctzll(m) : 0;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)own, first);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(own >> 32), first);
+    const uint64_t t = m ? (((uint64_t)hi << 32) | lo) : (uint64_t)(uintptr_t)g_zero_line;
+    return in ? own : t;
+}
+#ifndef NFCS_PAST
+#define NFCS_PAST 0
+#endif
+// NFCS_PAST 1 (measurement): past-frame lanes read the wave's row 0 frame start (tgt0) instead
+DEV uint64_t past_addr1(uint64_t own, bool in, uint64_t tgt0) {
+    if (NFCS_PAST == 1) return in ? own : tgt0;
+    return past_addr(own, in);
+}
+template <int NT>
+DEV uint4 ld16a(uint64_t a) {  // ld16 at a global address held as an integer (global_load, not flat)
+    const u32x4_t t = NT ? __builtin_nontemporal_load((gu32x4*)a) : *(gu32x4*)a;
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+
 // One row's packet, staged: frame window and its first K slots of chunks in flight.
 template <int K>
 struct RowStage {
@@ -697,7 +711,6 @@ struct RowStage {
     uint32_t valid, bad;
     uint32_t nh;    // fused L3 forward: next-hop index (row-uniform)
     uint32_t mis;   // 16-byte chunks between the frame start and the 128-byte line below it
-    const uint4* zl;  // the wave's zero chunk (zero_chunk): continuation loads past the frame
 };
 
 // Per-launch extras of update_rows_kernel: the fused L3 forward's inputs (unused by the plain
@@ -734,9 +747,10 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
-// (evict-first). Every load is always issued — lanes past the frame read zeros: from the wave's zero
-// chunk zl, or in the BUF shape (the update's short shape) through an out-of-range buffer offset with
-// no memory request (WaveBuf; zl again where a wave's frames span more than 4 GB) — so the waits are
+// (evict-first). Every load is always issued — lanes past the frame read the chunk of the
+// instruction's first in-frame lane (past_addr), or in the BUF shape (the update's short shape) zeros
+// through an out-of-range buffer offset with no memory request (WaveBuf; past_addr again where a
+// wave's frames span more than 4 GB) — so the waits are
 // counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
 // R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
 // each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
@@ -746,7 +760,7 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
 // profiles/r03_s3_ab_align*.jsonl). Without LA, mis = 0 and the windows are frame-relative.
 template <int K, int R = 16, bool FWD = false, bool LA = false, bool BUF = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, const uint4* zl,
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, uint64_t tgt0,
                    uint32_t nh = 0) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
@@ -759,7 +773,6 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
     S.len = live ? d.len : 0u;
     S.frame = arena + (live ? off : 0);
     S.mis = LA && live ? (uint32_t)(((uintptr_t)S.frame >> 4) & 7u) : 0u;
-    S.zl = zl;
     const uint32_t nch = (S.len + 15u) >> 4;
     const uint4* src = (const uint4*)S.frame;
     if (FWD) S.nh = nh;  // its MACs arrive as wave-uniform scalars (update_rows_kernel)
@@ -777,8 +790,8 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k - S.mis;
-            const uint4* a = (c < nch) ? src + c : zslot(zl, k);
-            S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
+            const uint64_t a = past_addr1((uint64_t)(uintptr_t)(src + c), c < nch, tgt0);
+            S.v[k] = k == 0 ? ld16a<0>(a) : ld16a<1>(a);
         }
     }
     // all K loads issue before any use of the header slot: without this fence the scheduler
@@ -855,6 +868,9 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     // frame chunk rl in lane rl: slot 0 itself when every row of the wave starts on a line
     uint4 h0 = S.v[0];
     if (LA && __builtin_amdgcn_ballot_w64(S.mis != 0) != 0) h0 = hdr_view<K, R>(S, rowbase4, rl);
+    // the header view past the frame reads zeros, as the plan expects: lanes past their frame loaded
+    // another frame's bytes (past_addr); the other slots' past-frame values are never summed
+    if (rl >= ((len + 15u) >> 4)) h0 = make_uint4(0u, 0u, 0u, 0u);
     // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
     // rewrite applied to the header registers, so the checksums below see the new header.
     bool fwd = false, tagged = false;
@@ -965,7 +981,7 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = cb + rlv + (uint32_t)R * k - S.mis;
-            w[k] = ld16<1>((c < nre) ? src + c : zslot(S.zl, k));
+            w[k] = ld16<1>((c < nre) ? src + c : g_zero_line);
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) acc_slot(acc, w[k], cb + rlv + (uint32_t)R * k - S.mis, lo4, re, tailfix);
@@ -1127,8 +1143,11 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     // forward's short-mix shape (+4-10%) measured slower with them and keep global loads
     // (profiles/r04_s2_wave_buf_ab.jsonl)
     constexpr bool BUF = !FWD && BS == 64 && R == 16;
+    const uint64_t off0 = ((uint64_t)D.w[0] - base16) * 16u;  // row 0: always a packet (pw < n)
+    const bool live0 = D.w[0] >= base16 && off0 + (((uint64_t)D.w[1] + 15u) & ~15ull) <= arena_bytes;
+    const uint64_t tgt0 = live0 ? (uint64_t)(uintptr_t)(arena + off0) : (uint64_t)(uintptr_t)g_zero_line;
     row_stage<K, R, FWD, LA, BUF>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl,
-                                  wave_buf<PW>(D, pw, n, arena, base16), zero_chunk(pw / PW), 0u);
+                                  wave_buf<PW>(D, pw, n, arena, base16), tgt0, 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
     if (FWD) {
 #pragma unroll
@@ -1138,7 +1157,7 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
         if (!(SF == SF_DEFER && defer)) {
 #pragma unroll
             for (uint32_t i = 0; i < PW; ++i) {
-                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)g_zero_pool;
+                const cu32* m = (q[i] < table_n) ? (const cu32*)(table + q[i]) : (const cu32*)g_zero_line;
                 wmac[3 * i] = m[0];
                 wmac[3 * i + 1] = m[1];
                 wmac[3 * i + 2] = m[2];
@@ -1657,12 +1676,12 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
     const uint32_t mis = (nl + lm <= KR || nl > KR) ? lm : 0u;
     const bool rot = LA && __builtin_amdgcn_ballot_w64(mis != 0) != 0;  // wave-uniform
 
-    const uint4* zl = zero_chunk(pw / PW);
+    const uint4* zl = g_zero_line;
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k - mis;  // frame chunk (wraps below the frame start)
-        v[k] = ld16<0>((c < nl) ? src + c : zslot(zl, k));
+        v[k] = ld16<0>((c < nl) ? src + c : zl);
     }
     // pop: the old dword after batch 0 (first dword of the window's chunk KR)
     const uint32_t nx0 = *(const uint32_t*)((KR - mis < nl) ? src + (KR - mis) : zl);
@@ -1760,7 +1779,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 #pragma unroll
             for (int k = 0; k < K2; ++k) {
                 const uint32_t c = cb + rlv + (uint32_t)R * k - mis;
-                w[k] = ld16<1>((c < nl) ? src + c : zslot(zl, k));
+                w[k] = ld16<1>((c < nl) ? src + c : zl);
             }
             const uint32_t nx = *(const uint32_t*)((cb + KR2 - mis < nl) ? src + (cb + KR2 - mis) : zl);
             vlan_edit<K2, R>(e, w, mode, rl, false, carry, nx, 0u, cb, wend, mis);
@@ -1899,7 +1918,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
     // line instead of two; round 3). Headers reaching past byte 47 (IPv6, IPv4 options) load chunks
     // 3..5 afterwards, lane by lane.
     const uint32_t rl = lane & 7u, r = lane >> 3;
-    const uint4* zl = zero_chunk(p0 / 64u);
+    const uint4* zl = g_zero_line;
     uint4 c[8];
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
@@ -1907,7 +1926,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
         const uint32_t qo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)dl.x);
         const uint32_t ql = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)len);
         const uint4* src = (const uint4*)(arena + (uint64_t)qo * 16u);
-        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : zslot(zl, (int)k));
+        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : zl);
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k)
@@ -2053,7 +2072,7 @@ __global__ __launch_bounds__(kBlock) void stream_read_kernel(const uint4* __rest
 #pragma unroll
     for (uint32_t k = 0; k < K; ++k) {
         const uint64_t i = base + 64u * k;
-        const uint4* a = i < n16 ? p + i : zero_chunk(w);
+        const uint4* a = i < n16 ? p + i : g_zero_line;
         v[k] = (MIX && k == 0) ? ld16<0>(a) : ld16<1>(a);
     }
     uint32_t acc = 0;
@@ -2120,12 +2139,12 @@ __global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __
     const bool live = pw + row < n && off + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes;
     const uint32_t nch = live ? (d.len + 15u) >> 4 : 0u;
     const uint4* src = (const uint4*)(arena + (live ? off : 0));
-    const uint4* zl = zero_chunk(pw / PW);
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k;
-        v[k] = k == 0 ? ld16<0>((c < nch) ? src + c : zslot(zl, k)) : ld16<1>((c < nch) ? src + c : zslot(zl, k));
+        const uint64_t a = past_addr((uint64_t)(uintptr_t)(src + c), c < nch);
+        v[k] = k == 0 ? ld16a<0>(a) : ld16a<1>(a);
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -2136,7 +2155,7 @@ __global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = cb + rl + (uint32_t)R * k;
-            w[k] = ld16<1>((c < nch) ? src + c : zslot(zl, k));
+            w[k] = ld16<1>((c < nch) ? src + c : g_zero_line);
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) acc ^= w[k].x ^ w[k].y ^ w[k].z ^ w[k].w;

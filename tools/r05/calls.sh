@@ -56,4 +56,18 @@ call_b() {
   done
 }
 
+call_c() {
+  # round 5, GPU call c: the GPU tests on the product (past-frame lanes read the chunk of the same
+  # instruction's first in-frame lane: no extra request), then the A/B: round 4's product (one 16-byte
+  # g_zero16), the product, the product with its data section moved (2304-byte pad), past-frame lanes
+  # aimed at the wave's row-0 frame start (NFCS_PAST=1) and at one page-aligned zero chunk (call b's
+  # z_single); C1, C3, the forward's C3 mix and the C4 shard, alternating on one box; then the default line
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5c && \
+  timeout -k 10 400 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5c/pytest.log 2>&1
+  local rc=$?; [ $rc -le 1 ] || return $rc
+  ab_lines gpurun_out/r5c 3 "nfcs_r4final cur cur_p2304 past_row0 z_single" \
+    "c1 --steps 50" "c3 --config 3 --steps 40" "fwdc3 --op l3fwd --config 3 --steps 40" "c4shard --packets 4194304 --steps 12" && \
+  timeout -k 10 300 python3 -u bench.py > gpurun_out/r5c/bench.json 2> gpurun_out/r5c/bench.err
+}
+
 "call_$1"
