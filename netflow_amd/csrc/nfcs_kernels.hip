@@ -48,9 +48,14 @@ DEV uint32_t xcd_block_n(uint32_t nblocks) {
 DEV uint32_t xcd_block() { return xcd_block_n(gridDim.x); }
 DEV uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// A zero line, 4 KB-aligned (its page offset never depends on what the linker puts before it): the
-// target of the loads past a frame where no frame line is at hand — VLAN, flow keys, continuation
-// batches of jumbo frames, the bench's stream reads, and instructions with no lane in its frame (past_addr).
+// The target of every load of a lane past its frame (or, in a line-aligned window, before it): every
+// load is issued by every lane, so a wave's compiler-counted vmcnt waits stay static. One zero line,
+// aligned to 4 KB, so its page offset never depends on what the linker places before it (round 4's
+// 16-byte g_zero16 sat wherever the linker put it). Round 5 measured the alternatives on one box,
+// alternating builds (profiles/r05_zero_target_ab.jsonl): one chunk per slot of a pool,
+// the same instruction's first in-frame chunk (no extra request, but ~12 more instructions per slot
+// ahead of the loads: C1 -2.5%, the C4 shard -2%), the wave's row-0 frame start — none faster; and the
+// forward's C3 mix moves by +-3% from run to run in every form, round 4's as well.
 __device__ __attribute__((aligned(4096))) uint4 g_zero_line[8];
 
 // Component j of a uint4 by mask arithmetic (no indexable temporary, so no scratch).
@@ -668,39 +673,6 @@ DEV WaveBuf wave_buf(const DescW<P>& D, uint64_t pw, uint32_t n, uint8_t* arena,
     return b;
 }
 
-// Where the row kernels' lanes past their frame load from (round 5). Every load is
-// issued by every lane, so the compiler's vmcnt waits stay counted, and a lane past its frame (or, in
-// a line-aligned window, before it) still needs an address. Round 4 aimed them all at one 16-byte
-// global: one extra request per load instruction, all of the chip's at one L2 channel per XCD, and the
-// fused forward's C3 mix moved between 0.68 and 0.75 ms per call with that global's link-time address
-// and from run to run. Now such a lane reads the chunk that the first in-frame lane of the SAME
-// instruction reads (ballot, find-first, two v_readlane): it adds no request at all; only an
-// instruction with no lane in its frame reads g_zero_line. Such lanes read another frame's bytes
-// instead of zeros: the sums never add them (they mask by region), and the header view the plan reads
-// is zeroed past the frame (row_process).
-typedef const __attribute__((address_space(1))) u32x4_t gu32x4;
-DEV uint64_t past_addr(uint64_t own, bool in) {
-    const uint64_t m = __builtin_amdgcn_ballot_w64(in);
-    const int first = m ? (int)__builtin_ctzll(m) : 0;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)own, first);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(own >> 32), first);
-    const uint64_t t = m ? (((uint64_t)hi << 32) | lo) : (uint64_t)(uintptr_t)g_zero_line;
-    return in ? own : t;
-}
-#ifndef NFCS_PAST
-#define NFCS_PAST 0
-#endif
-// NFCS_PAST 1 (measurement): past-frame lanes read the wave's row 0 frame start (tgt0) instead
-DEV uint64_t past_addr1(uint64_t own, bool in, uint64_t tgt0) {
-    if (NFCS_PAST == 1) return in ? own : tgt0;
-    return past_addr(own, in);
-}
-template <int NT>
-DEV uint4 ld16a(uint64_t a) {  // ld16 at a global address held as an integer (global_load, not flat)
-    const u32x4_t t = NT ? __builtin_nontemporal_load((gu32x4*)a) : *(gu32x4*)a;
-    return make_uint4(t.x, t.y, t.z, t.w);
-}
-
 // One row's packet, staged: frame window and its first K slots of chunks in flight.
 template <int K>
 struct RowStage {
@@ -747,10 +719,9 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are
 // parsed and, with inline stores, written back while still in L2), payload slots non-temporal
-// (evict-first). Every load is always issued — lanes past the frame read the chunk of the
-// instruction's first in-frame lane (past_addr), or in the BUF shape (the update's short shape) zeros
-// through an out-of-range buffer offset with no memory request (WaveBuf; past_addr again where a
-// wave's frames span more than 4 GB) — so the waits are
+// (evict-first). Every load is always issued — lanes past the frame read zeros: from g_zero_line, or
+// in the BUF shape (the update's short shape) through an out-of-range buffer offset with no memory
+// request (WaveBuf; g_zero_line again where a wave's frames span more than 4 GB) — so the waits are
 // counted vmcnt waits. Line-aligned windows (LA, round 3): lane rl of slot k holds the chunk
 // R*k + rl past the 128-byte line in which the frame starts, i.e. frame chunk R*k + rl - mis, so
 // each load instruction covers whole lines (2 for 16-lane rows, 1 for 8-lane rows) whatever the
@@ -760,8 +731,7 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
 // profiles/r03_s3_ab_align*.jsonl). Without LA, mis = 0 and the windows are frame-relative.
 template <int K, int R = 16, bool FWD = false, bool LA = false, bool BUF = false>
 DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const nfcs_desc& d,
-                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, uint64_t tgt0,
-                   uint32_t nh = 0) {
+                   uint64_t p64, uint32_t n, uint32_t base16, uint32_t rl, const WaveBuf& wb, uint32_t nh = 0) {
     const bool valid = p64 < n;
     const uint64_t off = ((uint64_t)d.off16 - base16) * 16u;
     const bool bad = valid && ((d.off16 < base16) ||
@@ -790,8 +760,8 @@ DEV void row_stage(RowStage<K>& S, uint8_t* arena, uint64_t arena_bytes, const n
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = rl + (uint32_t)R * k - S.mis;
-            const uint64_t a = past_addr1((uint64_t)(uintptr_t)(src + c), c < nch, tgt0);
-            S.v[k] = k == 0 ? ld16a<0>(a) : ld16a<1>(a);
+            const uint4* a = (c < nch) ? src + c : g_zero_line;
+            S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
         }
     }
     // all K loads issue before any use of the header slot: without this fence the scheduler
@@ -868,9 +838,6 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
     // frame chunk rl in lane rl: slot 0 itself when every row of the wave starts on a line
     uint4 h0 = S.v[0];
     if (LA && __builtin_amdgcn_ballot_w64(S.mis != 0) != 0) h0 = hdr_view<K, R>(S, rowbase4, rl);
-    // the header view past the frame reads zeros, as the plan expects: lanes past their frame loaded
-    // another frame's bytes (past_addr); the other slots' past-frame values are never summed
-    if (rl >= ((len + 15u) >> 4)) h0 = make_uint4(0u, 0u, 0u, 0u);
     // Fused L3 forward (switch.hpp:247-294): the decision, then the TTL decrement and MAC
     // rewrite applied to the header registers, so the checksums below see the new header.
     bool fwd = false, tagged = false;
@@ -1143,11 +1110,8 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     // forward's short-mix shape (+4-10%) measured slower with them and keep global loads
     // (profiles/r04_s2_wave_buf_ab.jsonl)
     constexpr bool BUF = !FWD && BS == 64 && R == 16;
-    const uint64_t off0 = ((uint64_t)D.w[0] - base16) * 16u;  // row 0: always a packet (pw < n)
-    const bool live0 = D.w[0] >= base16 && off0 + (((uint64_t)D.w[1] + 15u) & ~15ull) <= arena_bytes;
-    const uint64_t tgt0 = live0 ? (uint64_t)(uintptr_t)(arena + off0) : (uint64_t)(uintptr_t)g_zero_line;
     row_stage<K, R, FWD, LA, BUF>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl,
-                                  wave_buf<PW>(D, pw, n, arena, base16), tgt0, 0u);
+                                  wave_buf<PW>(D, pw, n, arena, base16), 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
     if (FWD) {
 #pragma unroll
@@ -2143,8 +2107,8 @@ __global__ __launch_bounds__(kBlock) void frames_read_kernel(const nfcs_desc* __
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = rl + (uint32_t)R * k;
-        const uint64_t a = past_addr((uint64_t)(uintptr_t)(src + c), c < nch);
-        v[k] = k == 0 ? ld16a<0>(a) : ld16a<1>(a);
+        const uint4* a = (c < nch) ? src + c : g_zero_line;
+        v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);
     }
     uint32_t acc = 0;
 #pragma unroll

@@ -70,4 +70,18 @@ call_c() {
   timeout -k 10 300 python3 -u bench.py > gpurun_out/r5c/bench.json 2> gpurun_out/r5c/bench.err
 }
 
+call_d() {
+  # round 5, GPU call d: the GPU tests on the product (one 4 KB-aligned zero line, call c's outcome); where
+  # the forward's C3-mix spread comes from (tools/r05/fwd_var.py: timing windows within one allocation
+  # against fresh allocations, the update beside it), the product and its inline segment stores past the
+  # caches (libfwd_nt); then the default bench line
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5d && \
+  timeout -k 10 400 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5d/pytest.log 2>&1
+  local rc=$?; [ $rc -le 1 ] || return $rc
+  timeout -k 10 300 python3 -u tools/r05/fwd_var.py --allocs 4 --windows 3 > gpurun_out/r5d/fwd_var_prod.jsonl 2> gpurun_out/r5d/fwd_var.err && \
+  NFCS_LIB=tools/r05/libfwd_nt.so timeout -k 10 300 python3 -u tools/r05/fwd_var.py --allocs 4 --windows 3 > gpurun_out/r5d/fwd_var_nt.jsonl 2>> gpurun_out/r5d/fwd_var.err && \
+  timeout -k 10 300 python3 -u tools/r05/fwd_var.py --allocs 3 --windows 3 --op update > gpurun_out/r5d/upd_var_prod.jsonl 2>> gpurun_out/r5d/fwd_var.err && \
+  timeout -k 10 300 python3 -u bench.py > gpurun_out/r5d/bench.json 2> gpurun_out/r5d/bench.err
+}
+
 "call_$1"
