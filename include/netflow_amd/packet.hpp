@@ -48,6 +48,26 @@
 
 namespace netflow_amd {
 
+namespace detail {
+// f(i0, i1) over [0, n) split across up to 8 threads for big bursts (the per-packet Packet ->
+// PacketBuffer loads of a burst of a million scattered objects take ~10 ms on one core); never throws:
+// a thread that cannot be started runs its range here.
+template <class F>
+void parallel_ranges(size_t n, F&& f) {
+    const size_t nt = n >= (size_t(1) << 16) ? 8 : 1;
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) {
+        try {
+            th.emplace_back([&f, n, t, nt] { f(n * t / nt, n * (t + 1) / nt); });
+        } catch (...) {
+            f(n * t / nt, n * (t + 1) / nt);
+        }
+    }
+    f(size_t(0), n / nt);
+    for (auto& x : th) x.join();
+}
+}  // namespace detail
+
 // The caller-facing contract of netflow::PacketBuffer (packet_buffer.hpp:10-111): the same
 // constructor arguments, accessors, ref_count and refcount calls, bool results of the window edits,
 // and exception types (std::invalid_argument from the constructor, std::out_of_range from
@@ -321,9 +341,8 @@ int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* 
     // then the transfers, then one scatter, one after the other)
     frames_.resize(n);
     lens_.resize(n);
-    // two dependent loads per packet (Packet -> PacketBuffer): split over a few threads for big bursts
     std::atomic<bool> too_long{false};
-    auto fill = [&](size_t i0, size_t i1) {
+    detail::parallel_ranges(n, [&](size_t i0, size_t i1) {
         for (size_t i = i0; i < i1; ++i) {
             auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
             const size_t len = b ? b->get_data_length() : 0;
@@ -331,18 +350,7 @@ int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* 
             frames_[i] = b ? b->get_data_start_ptr() : nullptr;
             lens_[i] = static_cast<uint32_t>(len);
         }
-    };
-    const size_t nt = n >= (size_t(1) << 16) ? 8 : 1;
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nt; ++t) {
-        try {
-            th.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
-        } catch (...) {  // no thread to be had: that range here (never throw)
-            fill(n * t / nt, n * (t + 1) / nt);
-        }
-    }
-    fill(0, n / nt);
-    for (auto& x : th) x.join();
+    });
     if (too_long.load()) return NFCS_EINVAL;
     return nfcs_update_host_frames(ctx_, frames_.data(), lens_.data(), static_cast<uint32_t>(n), status, 0);
 }
@@ -528,11 +536,12 @@ int ChecksumEngine::flow_keys_batch(Pkt* const* pkts, size_t n, nfcs_flow_key* k
 
 // Same interface as netflow::BufferPool (buffer_pool.hpp:57-123: allocate_buffer(payload,
 // headroom), free_buffer(buffer) with the PacketBuffer reference count), except that every
-// buffer up to slot_bytes is a slot of ONE pinned arena (nfcs_host_alloc). A burst whose buffers
-// come from the pool is checksummed with no gather copy: update_checksums_batch builds the
-// descriptors straight into the arena and calls nfcs_update_host on it (frames DMA'd from the
-// pinned arena, patch records back; or, with NFCS_HOST_ZERO_COPY, read by the kernel over PCIe
-// in place). Buffers larger than a slot are heap PacketBuffers, as the reference allocates them.
+// buffer up to slot_bytes is a slot of ONE pinned arena (nfcs_host_alloc). update_checksums_batch
+// builds the descriptors straight from the slots: frames that fill most of their slots go as spans
+// DMA'd from the pinned arena (nfcs_update_host, patch records back; or, with NFCS_HOST_ZERO_COPY,
+// read by the kernel over PCIe in place); frames that fill less than 85% of them are gathered by the
+// library's copy threads first (nfcs_update_host_frames), so the slots' unused bytes do not cross PCIe.
+// Buffers larger than a slot are heap PacketBuffers, as the reference allocates them.
 // The default slot is 2176 bytes (a 2048-byte data room + 128 bytes of headroom, DPDK's mbuf
 // layout): power-of-two slots alias on MI355X — C1's frames in 2048-byte slots checksum at 0.716 of
 // 8 TB/s (read pass 232 µs, write pass 41.7 µs) against 0.781 in 2176-byte slots (222 / 28.5 µs;
@@ -630,14 +639,22 @@ inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uin
     if (n == 0) return NFCS_OK;
     if (!pkts || n > 0xFFFFFFFFu) return NFCS_EINVAL;
     std::vector<nfcs_desc> desc(n);
+    std::atomic<bool> foreign{false};  // a packet whose buffer is not a 16-byte aligned slot of the pool
+    detail::parallel_ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
+            const unsigned char* d = b ? b->get_data_start_ptr() : nullptr;
+            if (!b || !in_arena(b) || ((d - arena_) & 15)) {
+                foreign.store(true, std::memory_order_relaxed);
+                break;
+            }
+            desc[i] = nfcs_desc{static_cast<uint32_t>((d - arena_) >> 4), static_cast<uint32_t>(b->get_data_length())};
+        }
+    });
+    if (foreign.load()) return eng_.update_checksums_batch(pkts, n, status);
     size_t drops = 0;  // places where the burst's arena offsets go down (a wrap of the pool's slots)
     uint64_t frame_bytes = 0;
     for (size_t i = 0; i < n; ++i) {
-        PacketBuffer* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
-        const unsigned char* d = b ? b->get_data_start_ptr() : nullptr;
-        if (!b || !in_arena(b) || ((d - arena_) & 15))
-            return eng_.update_checksums_batch(pkts, n, status);
-        desc[i] = nfcs_desc{static_cast<uint32_t>((d - arena_) >> 4), static_cast<uint32_t>(b->get_data_length())};
         drops += i && desc[i].off16 < desc[i - 1].off16;
         frame_bytes += desc[i].len;
     }
