@@ -84,4 +84,22 @@ call_d() {
   timeout -k 10 300 python3 -u bench.py > gpurun_out/r5d/bench.json 2> gpurun_out/r5d/bench.err
 }
 
+call_e() {
+  # round 5, GPU call e: the GPU tests on the product (the forward's 8-lane rows store their segments past
+  # the caches, call d's outcome); the product against the same with write-through segments (libfwd_wt)
+  # on the forward's C3 mix and on 1M x 64-byte frames (its tiny shape), alternating; the default line
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5e && \
+  timeout -k 10 400 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5e/pytest.log 2>&1
+  local rc=$?; [ $rc -le 1 ] || return $rc
+  ab_lines gpurun_out/r5e 3 "cur fwd_wt" "fwdc3 --op l3fwd --config 3 --steps 40" \
+    "fwdtiny --op l3fwd --config 0 --packets 1048576 --steps 40" && \
+  timeout -k 10 300 python3 -u bench.py > gpurun_out/r5e/bench.json 2> gpurun_out/r5e/bench.err
+}
+
+call_f() {
+  # round 5, GPU call f: rocprofv3 kernel stats of the default line and of each line alone, PMC traffic
+  # per call (tools/r05/prof_all.sh) on the final product
+  cd /root/repo && bash tools/r05/prof_all.sh r5f
+}
+
 "call_$1"
