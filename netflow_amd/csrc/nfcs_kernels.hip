@@ -998,12 +998,13 @@ DEV void row_process(const RowStage<K>& S, uint32_t rl, uint32_t rowbase4, uint8
             uint32_t last = 1u;
             if ((ipw & 0xFFFFu) != NFCS_PATCH_NONE) last = max(last, ((ipw & 0xFFFFu) + 1u) >> 4);
             if ((l4w & 0xFFFFu) != NFCS_PATCH_NONE) last = max(last, ((l4w & 0xFFFFu) + 1u) >> 4);
-            // 8-lane rows (the short-mix and tiny shapes) store past the caches (`sc0 sc1 nt`, as the
-            // update's short shape does), 16-lane rows write-through (`sc1`): round 5, calls rotating
-            // over fresh C3-mix batches, 0.690-0.702 against 0.719-0.728 ms per call
-            // (profiles/r05_fwd_var.jsonl); the replayed measurements of rounds 2-3 had seen no gain
+            // the short-mix shape (8-lane rows, line-aligned windows) stores past the caches (`sc0 sc1
+            // nt`, as the update's short shape does), the others write-through (`sc1`): round 5, calls
+            // rotating over fresh C3-mix batches, 0.690-0.710 against 0.719-0.735 ms per call
+            // (profiles/r05_fwd_var.jsonl, r05_fwd_store_ab.jsonl; the replayed measurements of rounds
+            // 2-3 had seen no gain); 1M x 64-byte frames (the tiny shape) 1% slower with them
             if ((!DFR || frame_stores) && rl <= last && 16u * rl < len) {
-                if (R == 8) st16_nt((uint4*)frame + rl, v);
+                if (R == 8 && LA) st16_nt((uint4*)frame + rl, v);
                 else st16<true>((uint4*)frame + rl, v);
             }
         }

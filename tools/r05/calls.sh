@@ -97,9 +97,12 @@ call_e() {
 }
 
 call_f() {
-  # round 5, GPU call f: rocprofv3 kernel stats of the default line and of each line alone, PMC traffic
-  # per call (tools/r05/prof_all.sh) on the final product
-  cd /root/repo && bash tools/r05/prof_all.sh r5f
+  # round 5, GPU call f: the update's tiny shape (8-lane rows) storing past the caches instead of
+  # write-through (libtiny_nt) on 1M x 64-byte frames, alternating; then rocprofv3 kernel stats of the
+  # default line and of each line alone, PMC traffic per call (tools/r05/prof_all.sh) on the product
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5f && \
+  ab_lines gpurun_out/r5f 3 "cur tiny_nt" "tiny --config 0 --packets 1048576 --steps 40" && \
+  bash tools/r05/prof_all.sh r5f
 }
 
 "call_$1"
