@@ -313,20 +313,59 @@ void host_block_free(HostBlock& b) {
     b = HostBlock{};
 }
 
-// memcpy split across the context's workers: one host thread copies pageable memory at ~15-25 GB/s,
+// Host copies whose destination this CPU does not read again (the staging slots, which the copy
+// engine reads next; frames copied back into a caller's arena): 16-byte non-temporal stores, so a
+// destination line is written once instead of first being read for ownership (a plain memcpy of a
+// 1500-byte frame moves 3 bytes over the memory bus per byte copied, this 2). Bytes before dst's
+// first 16-byte boundary and after its last go through plain stores; with zero_pad the last partial
+// chunk is instead stored whole, its bytes past len zeroed (the staged frames' 16-byte padding, which
+// the kernels read). Every worker that streamed calls nt_fence() before its part counts as done.
+typedef uint32_t host_u32x4 __attribute__((ext_vector_type(4)));
+static inline void stream_copy(uint8_t* dst, const uint8_t* src, uint64_t len, bool zero_pad) {
+    uint64_t k = std::min<uint64_t>(len, (16u - ((uintptr_t)dst & 15u)) & 15u);
+    if (k) memcpy(dst, src, k);
+    for (; k + 64 <= len; k += 64) {
+        host_u32x4 a, b, c, d;
+        memcpy(&a, src + k, 16); memcpy(&b, src + k + 16, 16);
+        memcpy(&c, src + k + 32, 16); memcpy(&d, src + k + 48, 16);
+        __builtin_nontemporal_store(a, (host_u32x4*)(dst + k));
+        __builtin_nontemporal_store(b, (host_u32x4*)(dst + k + 16));
+        __builtin_nontemporal_store(c, (host_u32x4*)(dst + k + 32));
+        __builtin_nontemporal_store(d, (host_u32x4*)(dst + k + 48));
+    }
+    for (; k + 16 <= len; k += 16) {
+        host_u32x4 a;
+        memcpy(&a, src + k, 16);
+        __builtin_nontemporal_store(a, (host_u32x4*)(dst + k));
+    }
+    if (k < len) {
+        if (zero_pad && !((uintptr_t)(dst + k) & 15u)) {
+            host_u32x4 t = {0u, 0u, 0u, 0u};
+            memcpy(&t, src + k, len - k);
+            __builtin_nontemporal_store(t, (host_u32x4*)(dst + k));
+        } else {
+            memcpy(dst + k, src + k, len - k);
+        }
+    }
+}
+static inline void nt_fence() { __builtin_ia32_sfence(); }  // the non-temporal stores drained
+
+// Copy split across the context's workers: one host thread copies pageable memory at ~15-25 GB/s,
 // below what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned). The
 // workers run on the GPU's NUMA node, next to the staging memory.
 void par_memcpy(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
     const size_t kMin = 4u << 20;
     if (bytes < 2 * kMin || c->workers.size() == 0) {
-        memcpy(dst, src, bytes);
+        stream_copy((uint8_t*)dst, (const uint8_t*)src, bytes, false);
+        nt_fence();
         return;
     }
     const size_t t = std::min<size_t>((size_t)c->workers.size() + 1, bytes / kMin);
     const size_t per = (bytes / t + 4095) & ~size_t(4095);
     c->workers.run((int)t, [&](int i) {
         const size_t o = (size_t)i * per;
-        if (o < bytes) memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o));
+        if (o < bytes) stream_copy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, bytes - o), false);
+        nt_fence();
     });
 }
 
@@ -951,9 +990,10 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
                     __builtin_prefetch(frames[i + j + kPf] + 128, 0, 0);
                 }
                 const uint64_t len = hd[j].len, o = (uint64_t)hd[j].off16 * 16u;
-                if (len) memcpy(dst + o, frames[i + j], len);
-                memset(dst + o + len, 0, pad(len) - len);  // the kernel reads whole 16-byte chunks
+                // the slot's 16-byte padding zeroed: the kernel reads whole 16-byte chunks
+                if (len) stream_copy(dst + o, frames[i + j], len, true);
             }
+            nt_fence();
         });
         hipStream_t st = c->hs[s];
         e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);

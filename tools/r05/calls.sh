@@ -105,4 +105,47 @@ call_f() {
   bash tools/r05/prof_all.sh r5f
 }
 
+call_g() {
+  # round 5, GPU call g (run inline, not from this file): the GPU tests, smoke() and the default bench
+  # line on the final product of session 2 (profiles/r05_g_*)
+  cd /root/repo && mkdir -p gpurun_out/r5g && \
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5g/pytest.log 2>&1 && \
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5g/smoke.log 2>&1 && \
+  timeout -k 10 240 python bench.py > gpurun_out/r5g/bench.json 2> gpurun_out/r5g/bench.err
+}
+
+call_h() {
+  # round 5, GPU call h: the host path's staging copies with non-temporal stores (the product: the
+  # scattered-frame gather and the pageable arena's staging copy) against plain memcpy (hostbase: the
+  # sources before that change, built by build_lib.sh into tools/r05/hostbase/libnfcs.so); the host
+  # GPU tests on the product first; then 3 alternating rounds of the adapter bench (1M C1 frames in
+  # separate PacketBuffers, the adapter / BufferPool paths) and of bench.py's host sub-line
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5h && \
+  timeout -k 10 300 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+    -k "host or adapter or pool or frames or ring" > gpurun_out/r5h/pytest.log 2>&1 || return 1
+  local r lib dir
+  for r in 1 2 3; do for lib in cur hostbase; do
+    dir=netflow_amd; [ "$lib" = cur ] || dir=tools/r05/$lib
+    LD_LIBRARY_PATH=$dir timeout -k 10 200 tests/cpp/_ref/netflow_adapter_test adapterbench 1048576 3 16 81cc3905092d7f44 \
+      > gpurun_out/r5h/adapter_${lib}_$r.json 2>> gpurun_out/r5h/adapter.err || return 1
+    NFCS_LIB=$dir/libnfcs.so timeout -k 10 300 python3 -u bench.py --no-cpu --no-replay --no-mix --no-c4 --steps 10 \
+      > gpurun_out/r5h/host_${lib}_$r.json 2>> gpurun_out/r5h/bench.err || return 1
+  done; done
+  # (as it ran, --no-c4 also skipped the host sub-line: only the adapter bench measured; call i repeats)
+}
+
+call_i() {
+  # round 5, GPU call i: call h again, with the host sub-line (bench.py without --no-c4; the line's C4
+  # shard runs too) and the adapter bench, 3 alternating rounds of product / hostbase
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5i || return 1
+  local r lib dir
+  for r in 1 2 3; do for lib in cur hostbase; do
+    dir=netflow_amd; [ "$lib" = cur ] || dir=tools/r05/$lib
+    LD_LIBRARY_PATH=$dir timeout -k 10 200 tests/cpp/_ref/netflow_adapter_test adapterbench 1048576 3 16 81cc3905092d7f44 \
+      > gpurun_out/r5i/adapter_${lib}_$r.json 2>> gpurun_out/r5i/adapter.err || return 1
+    NFCS_LIB=$dir/libnfcs.so timeout -k 10 300 python3 -u bench.py --no-cpu --no-replay --no-mix --steps 10 \
+      > gpurun_out/r5i/host_${lib}_$r.json 2>> gpurun_out/r5i/bench.err || return 1
+  done; done
+}
+
 "call_$1"
