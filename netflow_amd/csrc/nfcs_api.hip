@@ -534,8 +534,9 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
 // for a batch that fills its arena and can only over-estimate (frames never overlap). So a short
 // estimate is right, and only a long one can be wrong — a burst inside a larger ring. Then the call
 // also has its launch sample the frames' real footprint (sample_footprint, one wave, host-mapped
-// result), and the next call on the same descriptor array launches in the shape that sample says:
-// a NIC ring reusing its descriptor array adapts after one call, with no hint and no host sync.
+// result), and the next call on the same burst (descriptor array, n and arena_bytes; up to kObsSlots
+// bursts tracked, least recently used replaced) launches in the shape that sample says: a NIC ring
+// reusing its descriptor arrays adapts after one call, with no hint and no host sync.
 struct Shape { uint64_t mean; nfcs::ObsReq obs; };
 // The burst's observation slot, or -1 (no side effects).
 int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
