@@ -186,3 +186,27 @@ def test_scattered_small_bursts(engine):
     before = buf.copy()
     st = engine.update_host_frames(buf, offs, lens)
     assert (st == nf.ST_NONE).all() and np.array_equal(buf, before)
+
+
+@pytest.mark.parametrize("mode", ["patch", "frames"])
+@pytest.mark.parametrize("shift", [1, 8, 13])
+def test_pageable_arena_at_any_address(engine, mode, shift):
+    """A pageable arena that starts off a 16-byte boundary (a view `shift` bytes into a larger
+    buffer), 12K ring slots (26 MB: the staging copies split over the copy threads): the staging copy
+    in and, with whole frames back, the copy out store non-temporally only from the first 16-byte
+    boundary on (round 5). Results equal the oracle's; the guard bytes around the view stay."""
+    n_slots, n = 12_000, 11_000
+    frames = short_frames(47 + shift, n)
+    ring, desc = ring_burst(n_slots, 3_000, frames, 13 + shift)
+    ref = ring.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    big = np.random.default_rng(shift).integers(0, 256, ring.nbytes + 64, dtype=np.uint8)
+    guard = big.copy()
+    view = big[shift: shift + ring.nbytes]
+    view[:] = ring
+    assert view.ctypes.data % 16 == shift % 16
+    st = engine.update_host(view, desc, mode=mode)
+    assert np.array_equal(st, rst)
+    assert np.array_equal(view, ref)
+    assert np.array_equal(big[:shift], guard[:shift])
+    assert np.array_equal(big[shift + ring.nbytes:], guard[shift + ring.nbytes:])
