@@ -192,10 +192,11 @@ def test_scattered_small_bursts(engine):
 @pytest.mark.parametrize("shift", [1, 8, 13])
 def test_pageable_arena_at_any_address(engine, mode, shift):
     """A pageable arena that starts off a 16-byte boundary (a view `shift` bytes into a larger
-    buffer), 12K ring slots (26 MB: the staging copies split over the copy threads): the staging copy
+    buffer), 20K ring slots (43.5 MB: chunks of a quarter of the span, over 8 MiB, so each staging copy
+    splits over the copy threads): the staging copy
     in and, with whole frames back, the copy out store non-temporally only from the first 16-byte
     boundary on (round 5). Results equal the oracle's; the guard bytes around the view stay."""
-    n_slots, n = 12_000, 11_000
+    n_slots, n = 20_000, 19_000
     frames = short_frames(47 + shift, n)
     ring, desc = ring_burst(n_slots, 3_000, frames, 13 + shift)
     ref = ring.copy()
