@@ -16,7 +16,6 @@
 
 #include <algorithm>
 #include <condition_variable>
-#include <functional>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -61,13 +60,21 @@ public:
         quit_ = false;
     }
     int size() const { return (int)th_.size(); }
-    void run(int k, const std::function<void(int)>& fn) noexcept {
+    // fn is called by reference, never copied (no allocation: nothing here can throw)
+    template <class F>
+    void run(int k, const F& fn) noexcept {
         if (k <= 1 || th_.empty()) {
             for (int i = 0; i < k; ++i) fn(i);
             return;
         }
+        run_erased(k, [](const void* f, int i) { (*(const F*)f)(i); }, &fn);
+    }
+
+private:
+    void run_erased(int k, void (*call)(const void*, int), const void* fn) noexcept {
         std::unique_lock<std::mutex> l(mu_);
-        job_ = &fn;
+        call_ = call;
+        job_ = fn;
         parts_ = k;
         next_ = 0;
         pending_ = k;
@@ -77,14 +84,13 @@ public:
         done_.wait(l, [&] { return pending_ == 0; });
         job_ = nullptr;
     }
-
-private:
     void take(std::unique_lock<std::mutex>& l) {
         while (next_ < parts_) {
             const int i = next_++;
-            const std::function<void(int)>* f = job_;
+            void (*const call)(const void*, int) = call_;
+            const void* const f = job_;
             l.unlock();
-            (*f)(i);
+            call(f, i);
             l.lock();
             if (--pending_ == 0) done_.notify_all();
         }
@@ -103,7 +109,8 @@ private:
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
-    const std::function<void(int)>* job_ = nullptr;
+    void (*call_)(const void*, int) = nullptr;
+    const void* job_ = nullptr;
     int parts_ = 0, next_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
     bool quit_ = false;
