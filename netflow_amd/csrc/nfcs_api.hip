@@ -129,7 +129,8 @@ struct nfcs_ctx {
     static constexpr size_t kStageBytes = size_t(64) << 20;  // arena bytes per staging slot
     bool host_ready = false;  // every staging slot allocated (ensure_host_pipeline)
     hipStream_t hs[kSlots] = {nullptr, nullptr};
-    hipEvent_t done[kSlots] = {nullptr, nullptr};
+    hipEvent_t done[kSlots] = {nullptr, nullptr};    // a slot's chunk finished (records / frames back)
+    hipEvent_t staged[kSlots] = {nullptr, nullptr};  // a slot's host arena and descriptors copied in
     size_t stage_bytes = 0;   // arena bytes per slot
     uint32_t stage_pkts = 0;  // descriptors per slot
     int copy_threads = 8;     // host threads for pageable <-> pinned staging copies
@@ -383,6 +384,7 @@ void free_host_pipeline(nfcs_ctx* c) {
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
         if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+        if (c->staged[s]) (void)hipEventDestroy(c->staged[s]);
         (void)hipFree(c->d_arena[s]);
         (void)hipFree(c->d_desc[s]);
         (void)hipFree(c->d_status[s]);
@@ -390,6 +392,7 @@ void free_host_pipeline(nfcs_ctx* c) {
         host_block_free(c->hb[s]);
         c->hs[s] = nullptr;
         c->done[s] = nullptr;
+        c->staged[s] = nullptr;
         c->d_arena[s] = nullptr;
         c->d_desc[s] = nullptr;
         c->d_status[s] = nullptr;
@@ -436,6 +439,7 @@ int build_host_pipeline(nfcs_ctx* ctx) {
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         NFCS_HIP(hipStreamCreateWithFlags(&ctx->hs[s], hipStreamNonBlocking));
         NFCS_HIP(hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming));
+        NFCS_HIP(hipEventCreateWithFlags(&ctx->staged[s], hipEventDisableTiming));
         NFCS_HIP(hipMalloc(&ctx->d_arena[s], ctx->stage_bytes));
         NFCS_HIP(hipMalloc(&ctx->d_desc[s], a_desc));
         NFCS_HIP(hipMalloc(&ctx->d_status[s], ctx->stage_pkts));
@@ -826,21 +830,27 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint32_t m = k.i1 - k.i0;
         if (patch_only) {
             // each record writes into another frame's header line, which the DMA read but the
-            // CPU has not cached: prefetch the line kPf packets ahead so the misses overlap
-            constexpr uint32_t kPf = 16;
-            for (uint32_t i = 0; i < m; ++i) {
-                if (i + kPf < m) {
-                    const nfcs_patch& q = c->h_patch[s][i + kPf];
-                    const uint32_t o = q.ip_off != NFCS_PATCH_NONE ? q.ip_off : q.l4_off;
-                    const uint64_t a = (uint64_t)h_desc[k.i0 + i + kPf].off16 * 16u + (o & 0xFFC0u);
-                    if (a < arena_bytes) __builtin_prefetch(h_arena + a, 1, 0);
+            // CPU has not cached: prefetch the line kPf packets ahead so the misses overlap; large
+            // chunks over the workers
+            const nfcs_patch* pq = c->h_patch[s];
+            const int np = m >= 16384 ? c->workers.size() + 1 : 1;
+            c->workers.run(np, [&](int t) {
+                const uint32_t j0 = (uint32_t)((uint64_t)m * t / np), j1 = (uint32_t)((uint64_t)m * (t + 1) / np);
+                constexpr uint32_t kPf = 16;
+                for (uint32_t j = j0; j < j1; ++j) {
+                    if (j + kPf < j1) {
+                        const nfcs_patch& q = pq[j + kPf];
+                        const uint32_t o = q.ip_off != NFCS_PATCH_NONE ? q.ip_off : q.l4_off;
+                        const uint64_t a = (uint64_t)h_desc[k.i0 + j + kPf].off16 * 16u + (o & 0xFFC0u);
+                        if (a < arena_bytes) __builtin_prefetch(h_arena + a, 1, 0);
+                    }
+                    const nfcs_patch& pt = pq[j];
+                    if (!frame_end(k.i0 + j)) continue;
+                    uint8_t* f = h_arena + (uint64_t)h_desc[k.i0 + j].off16 * 16u;
+                    if (pt.ip_off != NFCS_PATCH_NONE) { f[pt.ip_off] = pt.ip[0]; f[pt.ip_off + 1] = pt.ip[1]; }
+                    if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
                 }
-                const nfcs_patch& pt = c->h_patch[s][i];
-                if (!frame_end(k.i0 + i)) continue;
-                uint8_t* f = h_arena + (uint64_t)h_desc[k.i0 + i].off16 * 16u;
-                if (pt.ip_off != NFCS_PATCH_NONE) { f[pt.ip_off] = pt.ip[0]; f[pt.ip_off + 1] = pt.ip[1]; }
-                if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
-            }
+            });
         } else if (!pinned) {
             par_memcpy(c, h_arena + k.base, c->h_arena[s], k.bytes);
         }
@@ -864,7 +874,15 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             end = ne;
             ++i1;
         }
-        finish(s);
+        // With patch records back, the slot's host arena and descriptors are free again once chunk
+        // k-2 has been copied in (`staged`), so chunk k's staging copy runs before chunk k-2's
+        // patches are applied and beside chunk k-1's transfer (round 5); with whole frames back the
+        // slot's arena receives them, and chunk k-2 is finished first
+        if (!patch_only) {
+            finish(s);
+        } else if (slot[s].used) {
+            e = hipEventSynchronize(c->staged[s]);
+        }
         if (e != hipSuccess) break;
         const uint32_t m = i1 - i;
         const uint64_t bytes = end - base;
@@ -874,11 +892,16 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             src = c->h_arena[s];
         }
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        if (patch_only) {
+            finish(s);  // chunk k-2's records and statuses are read out before chunk k's land
+            if (e != hipSuccess) break;
+        }
         hipStream_t st = c->hs[s];
         e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                            hipMemcpyHostToDevice, st);
         if (e == hipSuccess && bytes)
             e = hipMemcpyAsync(c->d_arena[s], src, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
         if (e == hipSuccess)
             e = nfcs::launch_update(c->di, c->d_arena[s], bytes, c->d_desc[s], m, (uint32_t)(base >> 4),
                                     c->d_status[s], patch_only ? c->d_patch[s] : nullptr,
@@ -916,23 +939,47 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!frames || !lens || flags != 0) return NFCS_EINVAL;
-    // every frame fits one staging slot (checked before anything is queued); a NULL frame is empty
-    auto flen = [&](uint32_t i) -> uint64_t { return frames[i] ? lens[i] : 0u; };
-    auto pad = [](uint64_t len) { return (len + 15u) & ~15ull; };
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (flen(i) > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
-        total += pad(flen(i));
-    }
     int rc = ensure_host_pipeline(c);
     if (rc) return rc;
-    // chunks of ~a quarter of the burst (at least 4 MiB, at most a staging slot), as nfcs_update_host
-    // cuts them, so that the gather of one chunk, the transfers and kernel of the previous one and
-    // the write-back of the one before overlap across the two slots
-    constexpr uint64_t kMinChunk = 4ull << 20;
-    const uint64_t chunk_target = std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max(kMinChunk, total / 4));
+    auto flen = [&](uint32_t i) -> uint64_t { return frames[i] ? lens[i] : 0u; };  // a NULL frame is empty
+    auto pad = [](uint64_t len) { return (len + 15u) & ~15ull; };
     const int parts = c->workers.size() + 1;
+    // every frame fits one staging slot (checked before anything is queued) and the burst's padded
+    // bytes, over the workers for large bursts (no serial pass over the burst on the caller's thread)
+    uint64_t chunk_target = 0;
+    {
+        constexpr int kMaxParts = 65;
+        uint64_t tot[kMaxParts] = {};
+        bool bad[kMaxParts] = {};
+        const int np = n >= 65536 ? std::min(parts, kMaxParts) : 1;
+        c->workers.run(np, [&](int t) {
+            const uint32_t j0 = (uint32_t)((uint64_t)n * t / np), j1 = (uint32_t)((uint64_t)n * (t + 1) / np);
+            uint64_t sum = 0;
+            bool b = false;
+            for (uint32_t j = j0; j < j1; ++j) {
+                const uint64_t l = flen(j);
+                b |= l > nfcs_ctx::kStageBytes;
+                sum += pad(l);
+            }
+            tot[t] = sum;
+            bad[t] = b;
+        });
+        uint64_t total = 0;
+        for (int t = 0; t < np; ++t) {
+            if (bad[t]) return NFCS_EINVAL;
+            total += tot[t];
+        }
+        // chunks of ~a quarter of the burst (at least 4 MiB, at most a staging slot), as
+        // nfcs_update_host cuts them
+        constexpr uint64_t kMinChunk = 4ull << 20;
+        chunk_target = std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max(kMinChunk, total / 4));
+    }
 
+    // The pipeline over the two slots, per chunk k in slot s: wait until chunk k-2's frames and
+    // descriptors have been copied in (`staged`: the slot's host arena is free again — not for its
+    // kernel and records, round 5), lay out chunk k's descriptors, gather its frames (the workers),
+    // then finish chunk k-2 (its records: checksum bytes written into the frames) and queue chunk
+    // k's copies, kernel and record copy. So the gather of chunk k runs beside the copy of chunk k-1.
     struct Chunk { uint32_t i0, i1; bool used; };
     Chunk slot[nfcs_ctx::kSlots] = {};
     hipError_t e = hipSuccess;
@@ -966,26 +1013,23 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
     uint32_t i = 0;
     int s = 0;
     while (i < n && e == hipSuccess) {
+        if (slot[s].used) {  // chunk k-2's copies in are done: its arena and descriptors are free
+            e = hipEventSynchronize(c->staged[s]);
+            if (e != hipSuccess) break;
+        }
         // next chunk: packets [i, i1), their 16-byte padded frames within chunk_target bytes (at
-        // least one) and the slot's descriptor room
+        // least one) and the slot's descriptor room, laid out back to back in the slot
+        nfcs_desc* hd = c->h_desc[s];
         uint32_t i1 = i;
         uint64_t bytes = 0;
         while (i1 < n && i1 - i < c->stage_pkts) {
-            const uint64_t b = bytes + pad(flen(i1));
+            const uint64_t l = flen(i1), b = bytes + pad(l);
             if (i1 > i && b > chunk_target) break;
+            hd[i1 - i] = nfcs_desc{(uint32_t)(bytes >> 4), (uint32_t)l};
             bytes = b;
             ++i1;
         }
-        finish(s);
-        if (e != hipSuccess) break;
         const uint32_t m = i1 - i;
-        // layout: frames back to back in the slot, 16-byte aligned; then the gather by the workers
-        nfcs_desc* hd = c->h_desc[s];
-        uint64_t off = 0;
-        for (uint32_t j = 0; j < m; ++j) {
-            hd[j] = nfcs_desc{(uint32_t)(off >> 4), (uint32_t)flen(i + j)};
-            off += pad(flen(i + j));
-        }
         uint8_t* dst = c->h_arena[s];
         const int ng = bytes >= (8u << 20) ? parts : 1;
         c->workers.run(ng, [&](int t) {
@@ -1003,9 +1047,12 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
             }
             nt_fence();
         });
+        finish(s);  // chunk k-2: its records and statuses are read out of the slot before chunk k's land
+        if (e != hipSuccess) break;
         hipStream_t st = c->hs[s];
         e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);
         if (e == hipSuccess && bytes) e = hipMemcpyAsync(c->d_arena[s], dst, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
         if (e == hipSuccess)
             e = nfcs::launch_update(c->di, c->d_arena[s], bytes ? bytes : 16, c->d_desc[s], m, 0u, c->d_status[s],
                                     c->d_patch[s], nullptr, nfcs::kUpdateRecords, st);

@@ -148,4 +148,32 @@ call_i() {
   done; done
 }
 
+call_l() {
+  # round 5, GPU call l (tools/r05/host_pipe and host_phases): the gather -> H2D pipeline without the
+  # kernel overlaps (28.8 ms for 1M C1 frames against 33.1 H2D alone), the product call took 35.1 ms
+  cd /root/repo && mkdir -p gpurun_out/r5l && \
+  timeout -k 10 300 tools/r05/host_pipe 1048576 5 8 > gpurun_out/r5l/pipe.json 2> gpurun_out/r5l/pipe.err && \
+  timeout -k 10 120 tools/r05/host_phases 1048576 5 > gpurun_out/r5l/phases.json 2> gpurun_out/r5l/phases.err
+}
+
+call_m() {
+  # round 5, GPU call m: the host pipelines wait for a slot's copies in (`staged`) instead of its whole
+  # chunk before staging the next one, validate scattered bursts over the workers and apply patch
+  # records over the workers (the product) against the sources before (hostbase2); the host GPU tests
+  # first; then 3 alternating rounds of host_phases, the adapter bench and bench.py's host sub-line
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5m && \
+  timeout -k 10 300 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+    -k "host or adapter or pool or frames or ring" > gpurun_out/r5m/pytest.log 2>&1 || return 1
+  local r lib dir
+  for r in 1 2 3; do for lib in cur hostbase2; do
+    dir=netflow_amd; [ "$lib" = cur ] || dir=tools/r05/$lib
+    LD_LIBRARY_PATH=$dir timeout -k 10 120 tools/r05/host_phases 1048576 5 > gpurun_out/r5m/phases_${lib}_$r.json \
+      2>> gpurun_out/r5m/phases.err || return 1
+    LD_LIBRARY_PATH=$dir timeout -k 10 200 tests/cpp/_ref/netflow_adapter_test adapterbench 1048576 3 16 81cc3905092d7f44 \
+      > gpurun_out/r5m/adapter_${lib}_$r.json 2>> gpurun_out/r5m/adapter.err || return 1
+    NFCS_LIB=$dir/libnfcs.so timeout -k 10 300 python3 -u bench.py --no-cpu --no-replay --no-mix --steps 10 \
+      > gpurun_out/r5m/host_${lib}_$r.json 2>> gpurun_out/r5m/bench.err || return 1
+  done; done
+}
+
 "call_$1"
