@@ -424,6 +424,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the C4-shard sub-line")
     ap.add_argument("--no-host", action="store_true", help="N = 1: skip the host-memory (PCIe) sub-line")
     ap.add_argument("--no-mix", action="store_true", help="N = 1: skip the C3-mix sub-lines (update, fused forward)")
+    ap.add_argument("--no-ops", action="store_true",
+                    help="N = 1: skip the C2 / forward / VLAN / flow-key sub-lines (child bench runs)")
     ap.add_argument("--op", choices=["update", "l3fwd", "flowkey", "vlan"], default="update")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -770,6 +772,8 @@ def main():
             out["host"] = host_line(eng, args, n)
             if host_adapter is not None:
                 out["host_adapter"] = host_adapter
+        if not args.no_ops:
+            out["more"] = more_lines(args)
     if rank == 0 and ws == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads, args.cpu_seconds, args.op)
     elif rank == 0:
@@ -1024,6 +1028,42 @@ def host_line(eng, args, n, reps: int = 3):
     out["gpu_numa_node"], out["staging_numa_local"] = node, local
     out["parity"] = {"reference_digest": want, "match": ok}
     return out
+
+
+# The other bench lines of DESIGN.md's scope table, each run as its own child bench.py (its own
+# process, warm-up, rotation, HIP events and reference digest) after the default line's own work, so
+# that the driver's run of the default line times them too ("every config other than C1
+# and the C4 shard is builder-run only"). name -> extra arguments.
+MORE_LINES = {
+    "c2": ["--config", "2", "--steps", "20"],
+    "l3fwd_c1": ["--op", "l3fwd", "--steps", "20"],
+    "l3fwd_4m": ["--op", "l3fwd", "--packets", "4194304", "--steps", "12"],
+    "vlan_c1": ["--op", "vlan", "--steps", "24"],
+    "flowkey_c1": ["--op", "flowkey", "--steps", "50"],
+}
+
+
+def more_lines(args):
+    """MORE_LINES, each a child `bench.py <args> --no-cpu --no-replay --no-c4 --no-host --no-mix
+    --no-ops` on this GPU, summarised: its value, ms per call, roofline frac and kernel time, parity.
+    A child that fails is reported as such; the default line is unaffected."""
+    res = {}
+    common = ["--no-cpu", "--no-replay", "--no-c4", "--no-host", "--no-mix", "--no-ops",
+              "--warmup", str(args.warmup), "--align", str(args.align)]
+    for name, extra in MORE_LINES.items():
+        cmd = [sys.executable, os.path.abspath(__file__), *extra, *common]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            res[name] = {"error": repr(e)[:300]}
+            continue
+        rf = d.get("roofline", {})
+        res[name] = {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
+                     "ms_per_step": d["ms_per_step"], "kernel_ms": rf.get("kernel_ms"), "frac": rf.get("frac"),
+                     "batches_rotated": rf.get("batches_rotated"), "parity": d.get("parity"),
+                     "args": " ".join(extra)}
+    return res
 
 
 def host_adapter_line(n: int):

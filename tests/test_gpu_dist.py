@@ -60,7 +60,7 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8", "--warmup", "2",
-           "--cpu-seconds", "1"]
+           "--cpu-seconds", "1", "--no-ops"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
@@ -85,6 +85,25 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     assert max(x["threads"] for x in cb["runs"]) == cb["nproc"] == len(os.sched_getaffinity(0))
     sc = d["stream_ceiling"]
     assert sc["read_only_GBps"] == max(sc["forms_GBps"].values())
+
+
+@pytest.mark.timeout(300)
+def test_one_gpu_line_carries_the_other_scope_lines():
+    """The N = 1 line's `more` sub-lines (round 5): C2, the fused forward on C1 and on 4M frames,
+    VLAN push/pop and flow keys, each a child bench run with its own rotation and HIP events, each
+    result's digest the reference's (the flow keys: their 64-byte records)."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "1",
+           "--no-cpu", "--no-replay", "--no-mix", "--no-host"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
+    more = d["more"]
+    assert set(more) == {"c2", "l3fwd_c1", "l3fwd_4m", "vlan_c1", "flowkey_c1"}, more
+    for k, v in more.items():
+        assert "error" not in v, (k, v)
+        assert v["parity"]["match"] is True and 0.2 < v["frac"] < 1.0 and v["value"] > 0, (k, v)
 
 
 def test_two_ranks_strong_split_c3():
