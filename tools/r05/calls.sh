@@ -176,4 +176,22 @@ call_m() {
   done; done
 }
 
+call_n() {
+  # round 5, GPU call n (run inline): the bench tests of the N = 1 line with its new `more` sub-lines
+  # (child runs of C2, forward C1 / 4M, VLAN, flow keys), then the default line (profiles/r05_n_*)
+  cd /root/repo && mkdir -p gpurun_out/r5n && \
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread -k "one_gpu" \
+    > gpurun_out/r5n/pytest.log 2>&1 && \
+  timeout -k 10 300 python bench.py > gpurun_out/r5n/bench.json 2> gpurun_out/r5n/bench.err
+}
+
+call_o() {
+  # round 5, GPU call o: the fused forward's short-mix shape as 16-lane rows at 7 waves/SIMD (the
+  # update's short shape) with buffer loads (libfwd16buf) or global loads (libfwd16), segment stores
+  # past the caches (tools/r05/fwd16_exp.py), against the product's 8-lane rows of 12 slots; the
+  # forward on the C3 mix, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5o && \
+  ab_lines gpurun_out/r5o 3 "cur fwd16buf fwd16" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
+
 "call_$1"
