@@ -789,9 +789,11 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint64_t e = o + (((uint64_t)h_desc[i].len + 15u) & ~15ull);
         return e <= arena_bytes ? e : 0;
     };
+    bool ordered = true;  // ascending offsets: the chunks' spans are disjoint
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t e = frame_end(i);
         if (e && e - (uint64_t)h_desc[i].off16 * 16u > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
+        ordered = ordered && (i == 0 || h_desc[i].off16 >= h_desc[i - 1].off16);
     }
     const uint64_t span = run_span(h_desc, 0, n, arena_bytes);
     int rc = ensure_host_pipeline(c);
@@ -851,8 +853,21 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                     if (pt.l4_off != NFCS_PATCH_NONE) { f[pt.l4_off] = pt.l4[0]; f[pt.l4_off + 1] = pt.l4[1]; }
                 }
             });
-        } else if (!pinned) {
+        } else if (ordered && !pinned) {
             par_memcpy(c, h_arena + k.base, c->h_arena[s], k.bytes);
+        } else if (!ordered) {
+            // Frames in any order: a chunk's span can hold frames of other chunks, staged before an
+            // earlier chunk wrote them back, so only the chunk's own frames are copied back (from
+            // the slot, where the frames came back also for a pinned arena)
+            const int np = m >= 16384 ? c->workers.size() + 1 : 1;
+            c->workers.run(np, [&](int t) {
+                for (uint32_t j = (uint32_t)((uint64_t)m * t / np); j < (uint32_t)((uint64_t)m * (t + 1) / np); ++j) {
+                    const uint32_t q = k.i0 + j;
+                    if (!frame_end(q)) continue;
+                    const uint64_t o = (uint64_t)h_desc[q].off16 * 16u;
+                    memcpy(h_arena + o, c->h_arena[s] + (o - k.base), h_desc[q].len);
+                }
+            });
         }
         if (h_status) memcpy(h_status + k.i0, c->h_status[s], m);
     };
@@ -912,7 +927,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                 e = hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch),
                                    hipMemcpyDeviceToHost, st);
             else if (bytes)
-                e = hipMemcpyAsync(pinned ? h_arena + base : c->h_arena[s], c->d_arena[s], bytes,
+                e = hipMemcpyAsync(pinned && ordered ? h_arena + base : c->h_arena[s], c->d_arena[s], bytes,
                                    hipMemcpyDeviceToHost, st);
         }
         if (e == hipSuccess && h_status)

@@ -69,9 +69,12 @@ def test_ring_burst_that_wraps(engine, mode):
     assert np.array_equal(got, ref)
 
 
-def test_ring_burst_wrapping_several_times_in_short_runs(engine):
-    """A burst whose descriptors jump back every few frames (runs of 1..64 ascending frames, each run
-    starting below the last): each run is staged as its own span, every result the oracle's."""
+@pytest.mark.parametrize("mode", ["patch", "frames"])
+def test_ring_burst_wrapping_several_times_in_short_runs(engine, mode):
+    """A burst whose descriptors jump back every few frames (runs of 1..64 ascending frames at random
+    places of the ring): a chunk is cut where an offset drops, so chunks' spans interleave — each
+    chunk's span can hold frames of the chunks beside it. Every result the oracle's, also with whole
+    frames back (only a chunk's own frames are copied back then)."""
     n_slots, n = 1 << 17, 60_000
     frames = short_frames(43, n)
     rng = np.random.default_rng(5)
@@ -93,7 +96,7 @@ def test_ring_burst_wrapping_several_times_in_short_runs(engine):
             j += 1
     ref = ring.copy()
     rst, _ = oracle.update_batch(ref, desc, nthreads=8)
-    st = engine.update_host(ring, desc)
+    st = engine.update_host(ring, desc, mode=mode)
     assert np.array_equal(st, rst)
     assert np.array_equal(ring, ref)
 
