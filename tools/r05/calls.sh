@@ -194,4 +194,19 @@ call_o() {
   ab_lines gpurun_out/r5o 3 "cur fwd16buf fwd16" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
 
+call_r() {
+  # round 5, GPU call r: the flow-key kernel's header-line loads with other cache policies (nt / sc1 /
+  # sc0 sc1 / sc0 sc1 nt; tools/r05/fk_exp.py) against the default: 3 alternating rounds of the
+  # flow-key line (C1 1M, 4 rotated batches, digest of the records), then per library the PMC
+  # traffic of one call (tools/pmc_traffic.py: FETCH_SIZE, WRITE_SIZE, EA read requests incl. 32-byte)
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5r && \
+  ab_lines gpurun_out/r5r 3 "cur fk_nt fk_sc1 fk_sc fk_scnt" "fk --op flowkey --steps 50" || return 1
+  local lib path
+  for lib in cur fk_nt fk_sc1 fk_sc fk_scnt; do
+    path=tools/r05/lib$lib.so; [ "$lib" = cur ] && path=netflow_amd/libnfcs.so
+    NFCS_LIB=$path timeout -k 10 200 python3 -u tools/pmc_traffic.py --out gpurun_out/r5r/pmc_$lib --configs 1 \
+      --ops flowkey --steps 5 > gpurun_out/r5r/pmc_$lib.log 2>&1 || return 1
+  done
+}
+
 "call_$1"
