@@ -1888,7 +1888,9 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
     // ports) in 8-lane rows: instruction k, row r -> packet 8k + r, lane rl -> chunk rl (0..2). A
     // frame starting up to 80 bytes into a 128-byte line reads that one line (64-byte starts: one
     // line instead of two; round 3). Headers reaching past byte 47 (IPv6, IPv4 options) load chunks
-    // 3..5 afterwards, lane by lane.
+    // 3..5 afterwards, lane by lane. The header lines load non-temporally (round 5, calls rotating
+    // over fresh batches, same box: 0.0385-0.0390 against 0.0411-0.0414 ms per 1M C1 frames; `sc1` /
+    // `sc0 sc1` loads measured as the default; profiles/r05_flowkey_load_policy_ab.jsonl).
     const uint32_t rl = lane & 7u, r = lane >> 3;
     const uint4* zl = g_zero_line;
     uint4 c[8];
@@ -1898,7 +1900,7 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
         const uint32_t qo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)dl.x);
         const uint32_t ql = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4u), (int)len);
         const uint4* src = (const uint4*)(arena + (uint64_t)qo * 16u);
-        c[k] = ld16<0>((rl < 3u && rl * 16u < ql) ? src + rl : zl);
+        c[k] = ld16<1>((rl < 3u && rl * 16u < ql) ? src + rl : zl);
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k)
