@@ -209,4 +209,17 @@ call_r() {
   done
 }
 
+call_s() {
+  # round 5, GPU call s: load cache policies under rotation (tools/r05/pol_exp.py): the row kernels'
+  # header slot non-temporal (upd_hdrnt), VLAN's loads non-temporal (vlan_nt; slots 1.. only:
+  # vlan_nt1), against the product (flow keys' header loads already nt); C1, C3, the forward's C3
+  # mix, VLAN C1, 3 alternating rounds; then the flow-key PMC traffic of the product (absolute library
+  # paths: pmc_traffic runs rocprofv3 from /tmp)
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5s && \
+  ab_lines gpurun_out/r5s 3 "cur upd_hdrnt vlan_nt vlan_nt1" "c1 --steps 50" "c3 --config 3 --steps 40" \
+    "fwdc3 --op l3fwd --config 3 --steps 40" "vlan --op vlan --steps 24" && \
+  NFCS_LIB=$PWD/netflow_amd/libnfcs.so timeout -k 10 200 python3 -u tools/pmc_traffic.py --out gpurun_out/r5s/pmc_cur \
+    --configs 1 --ops flowkey --steps 5 > gpurun_out/r5s/pmc_cur.log 2>&1
+}
+
 "call_$1"

@@ -1,0 +1,39 @@
+"""Measurement builds (not product): load cache policies under rotation (round 5; the flow-key
+kernel's header lines measured 6% faster non-temporal, profiles/r05_flowkey_load_policy_ab.jsonl):
+  upd_hdrnt  the row kernels' header slot (slot 0: update, forward) non-temporal like the payload slots
+  vlan_nt    every VLAN frame load non-temporal
+  vlan_nt1   VLAN's slots 1.. non-temporal, slot 0 default
+Builds tools/r05/lib<variant>.so through build_lib.sh. Run here: python3 tools/r05/pol_exp.py."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+SRC = os.path.join(ROOT, "netflow_amd", "csrc")
+EDITS = {
+    "upd_hdrnt": [("const u32x4_t t = k == 0 ? __builtin_amdgcn_raw_buffer_load_b128(wb.rs, vo, 0, 0)",
+                   "const u32x4_t t = k == 0 ? __builtin_amdgcn_raw_buffer_load_b128(wb.rs, vo, 0, kCpolNt)"),
+                  ("            S.v[k] = k == 0 ? ld16<0>(a) : ld16<1>(a);",
+                   "            S.v[k] = ld16<1>(a);")],
+    "vlan_nt": [("        v[k] = ld16<0>((c < nl) ? src + c : zl);",
+                 "        v[k] = ld16<1>((c < nl) ? src + c : zl);")],
+    "vlan_nt1": [("        v[k] = ld16<0>((c < nl) ? src + c : zl);",
+                  "        v[k] = k == 0 ? ld16<0>((c < nl) ? src + c : zl) : ld16<1>((c < nl) ? src + c : zl);")],
+}
+
+for name in sys.argv[1:] or EDITS:
+    tmp = tempfile.mkdtemp()
+    for f in ("nfcs_kernels.hip", "nfcs_api.hip", "nfcs_internal.h"):
+        shutil.copy(os.path.join(SRC, f), tmp)
+    p = os.path.join(tmp, "nfcs_kernels.hip")
+    s = open(p).read()
+    for a, b in EDITS[name]:
+        assert s.count(a) == 1, (name, a)
+        s = s.replace(a, b)
+    open(p, "w").write(s)
+    subprocess.run(["bash", os.path.join(ROOT, "tools/r05/build_lib.sh"), f"tools/r05/lib{name}.so"],
+                   env=dict(os.environ, SRC=tmp), check=True, cwd=ROOT)
+    shutil.rmtree(tmp)
+    print(name, "built")
