@@ -222,4 +222,14 @@ call_s() {
     --configs 1 --ops flowkey --steps 5 > gpurun_out/r5s/pmc_cur.log 2>&1
 }
 
+call_t() {
+  # round 5, GPU call t: rocprofv3 kernel stats of the flow-key line on the product with non-temporal
+  # header loads, and of the default line (--no-ops: its child lines are profiled alone above)
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5t && \
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r5t/flowkey" -o flowkey -- \
+    python3 bench.py --op flowkey --steps 50 --no-cpu > gpurun_out/r5t/flowkey.json 2> gpurun_out/r5t/flowkey.err && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r5t/default" -o default -- \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu --no-ops > gpurun_out/r5t/default.json 2> gpurun_out/r5t/default.err
+}
+
 "call_$1"
