@@ -232,4 +232,12 @@ call_t() {
     python3 bench.py --steps 20 --warmup 5 --no-cpu --no-ops > gpurun_out/r5t/default.json 2> gpurun_out/r5t/default.err
 }
 
+call_v() {
+  # round 5, GPU call v: store policies under rotation (tools/r05/pol_exp.py vlan_wt vlan_plain
+  # fk_recplain): VLAN's long-frame rows write-through / plain instead of past the caches, flow-key
+  # records plain instead of non-temporal; VLAN C1 and flow keys C1, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5v && \
+  ab_lines gpurun_out/r5v 3 "cur vlan_wt vlan_plain fk_recplain" "vlan --op vlan --steps 24" "fk --op flowkey --steps 50"
+}
+
 "call_$1"

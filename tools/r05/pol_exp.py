@@ -3,6 +3,7 @@ kernel's header lines measured 6% faster non-temporal, profiles/r05_flowkey_load
   upd_hdrnt  the row kernels' header slot (slot 0: update, forward) non-temporal like the payload slots
   vlan_nt    every VLAN frame load non-temporal
   vlan_nt1   VLAN's slots 1.. non-temporal, slot 0 default
+  vlan_wt / vlan_plain / fk_recplain   store policies (see EDITS)
 Builds tools/r05/lib<variant>.so through build_lib.sh. Run here: python3 tools/r05/pol_exp.py."""
 import os
 import shutil
@@ -21,6 +22,14 @@ EDITS = {
                  "        v[k] = ld16<1>((c < nl) ? src + c : zl);")],
     "vlan_nt1": [("        v[k] = ld16<0>((c < nl) ? src + c : zl);",
                   "        v[k] = k == 0 ? ld16<0>((c < nl) ? src + c : zl) : ld16<1>((c < nl) ? src + c : zl);")],
+    # store policies under rotation (call u): VLAN's long-frame rows write-through / plain instead of
+    # past the caches; the flow-key records plain instead of non-temporal
+    "vlan_wt": [("hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 16, true>)",
+                 "hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_WT, 16, true>)")],
+    "vlan_plain": [("hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_NT, 16, true>)",
+                    "hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_PLAIN, 16, true>)")],
+    "fk_recplain": [("            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)dst);",
+                     "            *(u32x4_t*)dst = u32x4_t{v.x, v.y, v.z, v.w};")],
 }
 
 for name in sys.argv[1:] or EDITS:
