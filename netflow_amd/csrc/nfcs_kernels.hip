@@ -1983,10 +1983,10 @@ __global__ __launch_bounds__(kBlock) void flow_keys_lanes_kernel(const nfcs_desc
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t q = 16u * j + (lane >> 2);  // packet of this 16-byte piece
         const uint4 v = *(const uint4*)(rows + q * kFkRow + 16u * (lane & 3u));
-        if (p0 + q < n) {
-            uint4* dst = (uint4*)(keys + p0 + q) + (lane & 3u);
-            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)dst);
-        }
+        // plain (write-back) stores: the L2 merges each 1 KB into whole lines (round 5, calls
+        // rotating over fresh batches, same box: 0.0352-0.0355 against 0.0387-0.0392 ms per 1M C1
+        // frames with non-temporal ones; profiles/r05_store_policy_ab.jsonl)
+        if (p0 + q < n) *((uint4*)(keys + p0 + q) + (lane & 3u)) = v;
     }
 }
 
@@ -1996,7 +1996,7 @@ hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t ar
     (void)di;
     if (n == 0) return hipSuccess;
     // 64 packets per wave, one lane each (round 3: C1 0.77 -> 0.82 against round 2's 8-lane rows of
-    // 4 slots; profiles/r03_s2_ab_flowkey_lanes.jsonl); non-temporal record stores, XCD-aware order
+    // 4 slots; profiles/r03_s2_ab_flowkey_lanes.jsonl); write-back record stores, XCD-aware order
     const uint32_t g = (n + 255u) / 256u;
     hipLaunchKernelGGL(flow_keys_lanes_kernel, dim3(g), dim3(kBlock), 0, stream, desc, n, g, arena, arena_bytes, keys,
                        hashes);
