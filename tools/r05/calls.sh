@@ -240,4 +240,12 @@ call_v() {
   ab_lines gpurun_out/r5v 3 "cur vlan_wt vlan_plain fk_recplain" "vlan --op vlan --steps 24" "fk --op flowkey --steps 50"
 }
 
+call_w() {
+  # round 5, GPU call w: the update's inline checksum-byte stores under rotation (tools/r05/pol_exp.py
+  # c3_wt c3_plain): the short shape write-through instead of past the caches; every inline store
+  # plain; C3, 1M x 64-byte frames (tiny shape) and C1, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5w && \
+  ab_lines gpurun_out/r5w 3 "cur c3_wt c3_plain" "c3 --config 3 --steps 40" "tiny --config 0 --packets 1048576 --steps 40" "c1 --steps 50"
+}
+
 "call_$1"

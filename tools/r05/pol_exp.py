@@ -30,6 +30,12 @@ EDITS = {
                     "hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_PLAIN, 16, true>)")],
     "fk_recplain": [("            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, (u32x4_t*)dst);",
                      "            *(u32x4_t*)dst = u32x4_t{v.x, v.y, v.z, v.w};")],
+    # the update's inline checksum-byte stores (call w): the short shape write-through (c3_wt) instead
+    # of past the caches; every inline store plain (c3_plain: short shape and tiny shape)
+    "c3_wt": [("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, false,")],
+    "c3_plain": [("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, false,"),
+                 ("                else st8<true>(frame + pos, w >> (16 + 8 * (rl & 1u)));",
+                  "                else st8<false>(frame + pos, w >> (16 + 8 * (rl & 1u)));")],
 }
 
 for name in sys.argv[1:] or EDITS:
