@@ -248,4 +248,13 @@ call_w() {
   ab_lines gpurun_out/r5w 3 "cur c3_wt c3_plain" "c3 --config 3 --steps 40" "tiny --config 0 --packets 1048576 --steps 40" "c1 --steps 50"
 }
 
+call_x() {
+  # round 5, GPU call x: block orders (tools/r05/pol_exp.py wp_xcd fk_noxcd vlan_xcd): the write passes
+  # in the read pass's XCD-aware order; flow keys in dispatch order; VLAN XCD-aware; C1, the C4 shard,
+  # the forward on 4M frames (deferred: apply_fwd_kernel), flow keys, VLAN; 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5x && \
+  ab_lines gpurun_out/r5x 3 "cur wp_xcd fk_noxcd vlan_xcd" "c1 --steps 50" "c4shard --packets 4194304 --steps 12" \
+    "fwd4m --op l3fwd --packets 4194304 --steps 12" "fk --op flowkey --steps 50" "vlan --op vlan --steps 24"
+}
+
 "call_$1"

@@ -36,6 +36,31 @@ EDITS = {
     "c3_plain": [("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, false,"),
                  ("                else st8<true>(frame + pos, w >> (16 + 8 * (rl & 1u)));",
                   "                else st8<false>(frame + pos, w >> (16 + 8 * (rl & 1u)));")],
+    # block orders (call x): the write passes in the read pass's XCD-aware order, so each XCD's write
+    # pass reads the records and descriptors its own read pass left in its L2 (wp_xcd); flow keys in
+    # dispatch order (fk_noxcd); VLAN in the XCD-aware order (vlan_xcd)
+    "wp_xcd": [("__global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict__ arena,\n"
+                "                                                             const nfcs_desc* __restrict__ desc,\n"
+                "                                                             uint32_t n, uint32_t base16,\n"
+                "                                                             const nfcs_patch* __restrict__ rec) {\n"
+                "    const uint32_t lane = threadIdx.x & 63u;\n"
+                "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;",
+                "__global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict__ arena,\n"
+                "                                                             const nfcs_desc* __restrict__ desc,\n"
+                "                                                             uint32_t n, uint32_t base16,\n"
+                "                                                             const nfcs_patch* __restrict__ rec) {\n"
+                "    const uint32_t lane = threadIdx.x & 63u;\n"
+                "    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;"),
+               ("    const uint32_t lane = threadIdx.x & 63u;\n"
+                "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;\n"
+                "    const bool in = i < n;",
+                "    const uint32_t lane = threadIdx.x & 63u;\n"
+                "    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;\n"
+                "    const bool in = i < n;")],
+    "fk_noxcd": [("    const uint64_t p0 = ((uint64_t)xcd_block_n(nblocks) * kWavesPerBlock + rfl(wave)) * 64u;",
+                  "    const uint64_t p0 = ((uint64_t)blockIdx.x * kWavesPerBlock + rfl(wave)) * 64u;")],
+    "vlan_xcd": [("    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;",
+                  "    const uint64_t pw = (uint64_t)xcd_block() * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;")],
 }
 
 for name in sys.argv[1:] or EDITS:
