@@ -1226,7 +1226,10 @@ __global__ __launch_bounds__(kBlock) void apply_bytes_kernel(uint8_t* __restrict
                                                              uint32_t n, uint32_t base16,
                                                              const nfcs_patch* __restrict__ rec) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    // the read pass's XCD-aware order: each XCD writes the eighth of the sub-batch its own read pass
+    // covered, whose records and descriptors its L2 still holds (round 5, calls rotating over fresh
+    // batches: C1 -0.5%, the C4 shard -0.4% per call; profiles/r05_block_order_ab.jsonl)
+    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;
     const nfcs_desc d = i < n ? desc[i] : nfcs_desc{0u, 0u};
     // The record is loaded with the descriptor, before the decision — one memory round trip ahead
     // of the stores instead of two (C1 +1.5%, the 4M shard +0.5%; records of waves that stored
@@ -1280,7 +1283,7 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
                                                            const nfcs_nexthop* __restrict__ table,
                                                            const nfcs_patch* __restrict__ rec) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;  // as apply_bytes_kernel
     const bool in = i < n;
     const nfcs_desc d = in ? desc[i] : nfcs_desc{0u, 0u};
     const uint2 r0 = in ? ((const uint2*)rec)[i] : make_uint2(0xFFFFFFFFu, 0u);
