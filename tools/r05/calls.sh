@@ -257,4 +257,11 @@ call_x() {
     "fwd4m --op l3fwd --packets 4194304 --steps 12" "fk --op flowkey --steps 50" "vlan --op vlan --steps 24"
 }
 
+call_y() {
+  # round 5, GPU call y: the forward's short-mix segment stores plain instead of past the caches
+  # (tools/r05/pol_exp.py fwd_plain); the forward on the C3 mix, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5y && \
+  ab_lines gpurun_out/r5y 3 "cur fwd_plain" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
+
 "call_$1"

@@ -61,6 +61,9 @@ EDITS = {
                   "    const uint64_t p0 = ((uint64_t)blockIdx.x * kWavesPerBlock + rfl(wave)) * 64u;")],
     "vlan_xcd": [("    const uint64_t pw = (uint64_t)blockIdx.x * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;",
                   "    const uint64_t pw = (uint64_t)xcd_block() * (kBlock / R) + rfl(threadIdx.x >> 6) * PW;")],
+    # the forward's short-mix segment stores plain (write-back) instead of past the caches (call y)
+    "fwd_plain": [("                if (R == 8 && LA) st16_nt((uint4*)frame + rl, v);",
+                   "                if (R == 8 && LA) st16<false>((uint4*)frame + rl, v);")],
 }
 
 for name in sys.argv[1:] or EDITS:
