@@ -264,4 +264,12 @@ call_y() {
   ab_lines gpurun_out/r5y 3 "cur fwd_plain" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
 
+call_z() {
+  # round 5, GPU call z: the row kernels' read pass and the write passes in dispatch order instead of
+  # XCD-aware (tools/r05/pol_exp.py rp_noxcd); C1, C3, the C4 shard, the forward's C3 mix, 3 rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5z && \
+  ab_lines gpurun_out/r5z 3 "cur rp_noxcd" "c1 --steps 50" "c3 --config 3 --steps 40" \
+    "c4shard --packets 4194304 --steps 12" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
+
 "call_$1"

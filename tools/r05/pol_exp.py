@@ -64,6 +64,13 @@ EDITS = {
     # the forward's short-mix segment stores plain (write-back) instead of past the caches (call y)
     "fwd_plain": [("                if (R == 8 && LA) st16_nt((uint4*)frame + rl, v);",
                    "                if (R == 8 && LA) st16<false>((uint4*)frame + rl, v);")],
+    # the row kernels' read pass and the write passes in dispatch order instead of XCD-aware (call z)
+    "rp_noxcd": [("    const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (BS / R) + rfl(threadIdx.x >> 6) * PW;",
+                  "    const uint64_t pw = (uint64_t)blockIdx.x * (BS / R) + rfl(threadIdx.x >> 6) * PW;"),
+                 ("    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;  // as apply_bytes_kernel",
+                  "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // as apply_bytes_kernel"),
+                 ("    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;\n    const nfcs_desc d",
+                  "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;\n    const nfcs_desc d")],
 }
 
 for name in sys.argv[1:] or EDITS:
