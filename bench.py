@@ -1055,14 +1055,13 @@ def more_lines(args):
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
             d = json.loads(r.stdout.strip().splitlines()[-1])
-        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
-            res[name] = {"error": repr(e)[:300]}
-            continue
-        rf = d.get("roofline", {})
-        res[name] = {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
-                     "ms_per_step": d["ms_per_step"], "kernel_ms": rf.get("kernel_ms"), "frac": rf.get("frac"),
-                     "batches_rotated": rf.get("batches_rotated"), "parity": d.get("parity"),
-                     "args": " ".join(extra)}
+            rf = d.get("roofline", {})
+            res[name] = {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
+                         "ms_per_step": d["ms_per_step"], "kernel_ms": rf.get("kernel_ms"), "frac": rf.get("frac"),
+                         "batches_rotated": rf.get("batches_rotated"), "parity": d.get("parity"),
+                         "args": " ".join(extra)}
+        except (subprocess.TimeoutExpired, ValueError, IndexError, KeyError, TypeError, AttributeError) as e:
+            res[name] = {"error": repr(e)[:300], "args": " ".join(extra)}
     return res
 
 
