@@ -272,4 +272,12 @@ call_z() {
     "c4shard --packets 4194304 --steps 12" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
 
+call_aa() {
+  # round 5, GPU call aa: the update's short shape as 8-lane rows of 12 slots (the forward's short-mix
+  # form; round 3 measured it 6% slower on a replayed batch), stores write-through (c3r8) or past the
+  # caches (c3r8nt); C3 under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5aa && \
+  ab_lines gpurun_out/r5aa 3 "cur c3r8 c3r8nt" "c3 --config 3 --steps 40"
+}
+
 "call_$1"

@@ -71,6 +71,14 @@ EDITS = {
                   "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // as apply_bytes_kernel"),
                  ("    const uint64_t i = (uint64_t)xcd_block() * kBlock + threadIdx.x;\n    const nfcs_desc d",
                   "    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;\n    const nfcs_desc d")],
+    # the update's short shape as the forward's short-mix rows: 8-lane rows of 12 slots, line-aligned
+    # windows, 8 packets per one-wave workgroup at 6 waves/SIMD, stores write-through (c3r8) or past
+    # the caches (c3r8nt) (call aa)
+    "c3r8": [("        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);",
+              "        else if (shape == kShapeShort) launch_rows<12, 8, 6, 64, false, SF, 1, 12>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd);")],
+    "c3r8nt": [("        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);",
+                "        else if (shape == kShapeShort) launch_rows<12, 8, 6, 64, false, SF, 1, 12>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd);"),
+               ("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, !FWD && BS == 64,")],
 }
 
 for name in sys.argv[1:] or EDITS:
