@@ -280,4 +280,11 @@ call_aa() {
   ab_lines gpurun_out/r5aa 3 "cur c3r8 c3r8nt" "c3 --config 3 --steps 40"
 }
 
+call_ab() {
+  # round 5, GPU call ab: flow keys with descriptors loaded non-temporally (fk_descnt) / hashes stored
+  # non-temporally (fk_hashnt), against the product; C1 under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ab && \
+  ab_lines gpurun_out/r5ab 3 "cur fk_descnt fk_hashnt" "fk --op flowkey --steps 50"
+}
+
 "call_$1"

@@ -79,6 +79,12 @@ EDITS = {
     "c3r8nt": [("        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);",
                 "        else if (shape == kShapeShort) launch_rows<12, 8, 6, 64, false, SF, 1, 12>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd);"),
                ("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, !FWD && BS == 64,")],
+    # flow keys: descriptors loaded non-temporally (fk_descnt); hashes stored non-temporally (fk_hashnt)
+    # (call ab)
+    "fk_descnt": [("    if (p < n) dl = ((const uint2*)desc)[p];",
+                   "    if (p < n) { typedef uint32_t u32x2_t __attribute__((ext_vector_type(2))); const u32x2_t t_ = __builtin_nontemporal_load((const u32x2_t*)desc + p); dl = make_uint2(t_.x, t_.y); }")],
+    "fk_hashnt": [("    if (hashes && p < n) hashes[p] = hv;",
+                   "    if (hashes && p < n) __builtin_nontemporal_store(hv, hashes + p);")],
 }
 
 for name in sys.argv[1:] or EDITS:
