@@ -287,4 +287,12 @@ call_ab() {
   ab_lines gpurun_out/r5ab 3 "cur fk_descnt fk_hashnt" "fk --op flowkey --steps 50"
 }
 
+call_ac() {
+  # round 5, GPU call ac: VERDICT r4 item 2's test on the final product: the forward's C3 mix (and the
+  # update's C3) in the product and in two libraries whose data sections move g_zero_line by a page
+  # (PAD 1536 / 2304, build_lib.sh), 4 alternating rounds, each line its own process
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ac && \
+  ab_lines gpurun_out/r5ac 4 "cur cur_p1536 cur_p2304" "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40"
+}
+
 "call_$1"
