@@ -13,7 +13,7 @@ run() {  # name, bench args...
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/$name" -o $name -- \
     python3 bench.py "$@" > "$OUT/$name.json" 2> "$OUT/$name.err" || exit 1
 }
-run default --steps 20 --warmup 5 --no-cpu
+run default --steps 20 --warmup 5 --no-cpu --no-ops  # the `more` child lines are profiled alone below
 run c1 --steps 50 --no-cpu --no-replay --no-host --no-c4
 run c2 --config 2 --steps 30 --no-cpu --no-replay --no-host --no-c4
 run c3 --config 3 --steps 30 --no-cpu --no-replay --no-host --no-c4
