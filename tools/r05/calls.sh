@@ -295,4 +295,11 @@ call_ac() {
   ab_lines gpurun_out/r5ac 4 "cur cur_p1536 cur_p2304" "fwdc3 --op l3fwd --config 3 --steps 40" "c3 --config 3 --steps 40"
 }
 
+call_ad() {
+  # round 5, GPU call ad: the update's short shape in 256-thread workgroups (c3_wg256; round 3 chose
+  # one-wave workgroups on a replayed batch), C3 under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ad && \
+  ab_lines gpurun_out/r5ad 3 "cur c3_wg256" "c3 --config 3 --steps 40"
+}
+
 "call_$1"

@@ -85,6 +85,13 @@ EDITS = {
                    "    if (p < n) { typedef uint32_t u32x2_t __attribute__((ext_vector_type(2))); const u32x2_t t_ = __builtin_nontemporal_load((const u32x2_t*)desc + p); dl = make_uint2(t_.x, t_.y); }")],
     "fk_hashnt": [("    if (hashes && p < n) hashes[p] = hv;",
                    "    if (hashes && p < n) __builtin_nontemporal_store(hv, hashes + p);")],
+    # the update's short shape in 256-thread workgroups (4 waves on one CU share the descriptor line
+    # of their 16 packets through its scalar cache), buffer loads and nt stores kept (call ad)
+    "c3_wg256": [("    constexpr bool BUF = !FWD && BS == 64 && R == 16;",
+                  "    constexpr bool BUF = !FWD && R == 16 && (BS == 64 || !LA);"),
+                 ("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, !FWD && R == 16 && (BS == 64 || !LA),"),
+                 ("        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);",
+                  "        else if (shape == kShapeShort) launch_rows<6, 16, 7, kBlock, false, SF, 0, 6>(g4, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd);")],
 }
 
 for name in sys.argv[1:] or EDITS:
