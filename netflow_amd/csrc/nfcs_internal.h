@@ -60,8 +60,9 @@ constexpr uint32_t kSubBatchAbovePackets = 1u << 19;
 // rotating over fresh batches) the inline write-through segments cost 1M-packet C1 bursts as much as
 // the update's inline stores do.
 constexpr uint32_t kFwdDeferAbovePackets = kInlineMaxPackets;
-// Below this mean arena footprint per packet the checksum kernel runs in one-wave workgroups at
-// 7 waves/SIMD (C3 +2-3%); the shape changes speed only, never the store form.
+// Below this mean arena footprint per packet the checksum kernel runs the short shape (16-lane rows,
+// frame-relative windows, buffer loads, 7 waves/SIMD); the shape changes speed only, never the
+// store form.
 constexpr uint64_t kSmallMeanBytes = 1200;
 // Below this one it runs 8-lane rows, 8 packets per wave (short frames are packet-rate bound:
 // uniform 64-256 B frames 1.8-1.9x, IMIX 7:4:1 of 64/570/1500 B 1.47x, 768 B 1.2x; the C3 mix,

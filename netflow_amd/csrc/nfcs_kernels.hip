@@ -1112,12 +1112,13 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
     const bool frame_stores = SF == SF_INLINE || (SF == SF_DEFER && !defer);
     nfcs_patch* rec = patch ? patch : (defer ? ws : nullptr);
     RowStage<K> S;
-    // buffer loads in the plain update's short shape (16-lane rows, one-wave workgroups), where most
-    // lanes of a wave's later slots are past their frames: C3 0.689-0.692 -> 0.664-0.669 ms per call;
-    // the long shape (+0.5%), the C4 shard (+0.8%), the 8-lane tiny shape (+1.2%) and the fused
-    // forward's short-mix shape (+4-10%) measured slower with them and keep global loads
-    // (profiles/r04_s2_wave_buf_ab.jsonl)
-    constexpr bool BUF = !FWD && BS == 64 && R == 16;
+    // buffer loads in the plain update's short shape (16-lane rows, frame-relative windows), where
+    // most lanes of a wave's later slots are past their frames: C3 0.689-0.692 -> 0.664-0.669 ms per
+    // call; the long shape (+0.5%), the C4 shard (+0.8%), the 8-lane tiny shape (+1.2%) and the
+    // fused forward's short-mix shape (+4-10%) measured slower with them and keep global loads
+    // (profiles/r04_s2_wave_buf_ab.jsonl). (The long shape's frame-relative body is never launched:
+    // it runs line-aligned windows, LAM 1.)
+    constexpr bool BUF = !FWD && R == 16 && !LA;
     row_stage<K, R, FWD, LA, BUF>(S, arena, arena_bytes, pick_desc<PW>(D, row), pw + row, n, base16, rl,
                                   wave_buf<PW>(D, pw, n, arena, base16), 0u);
     uint32_t wmac[3 * PW];  // the wave's next-hop MACs: scalar loads, selected per row at use
@@ -1136,9 +1137,9 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
             }
         }
     }
-    // inline checksum stores past the caches in the short-frame shape (16-lane rows, one-wave
-    // workgroups), write-through elsewhere (see row_process)
-    row_process<K, R, FWD, !FWD && R == 16 && BS == 64, FWD && SF == SF_DEFER, LA>(S, rl, rowbase4, status, rec,
+    // inline checksum stores past the caches in the short-frame shape (16-lane rows, frame-relative
+    // windows), write-through elsewhere (see row_process)
+    row_process<K, R, FWD, !FWD && R == 16 && !LA, FWD && SF == SF_DEFER, LA>(S, rl, rowbase4, status, rec,
                                                                                  frame_stores, table_n, wmac, table);
 }
 
@@ -1343,7 +1344,7 @@ __global__ __launch_bounds__(kBlock) void apply_fwd_kernel(uint8_t* __restrict__
 //   kShapeTiny   (< kTinyMeanBytes)  8-lane rows of 6 slots (768 B per row pass), 8 packets per
 //                one-wave workgroup: frames this short are packet-rate bound, and twice the packets
 //                per wave doubles it (64-256 B frames 1.8-1.9x, IMIX 1.47x, 768 B 1.2x);
-//   kShapeShort  (< kSmallMeanBytes) 16-lane rows in one-wave workgroups at 7 waves/SIMD: mixes of
+//   kShapeShort  (< kSmallMeanBytes) 16-lane rows in 256-thread workgroups at 7 waves/SIMD: mixes of
 //                short and long frames (C3), where 8-lane rows would need a second row pass for
 //                most waves (C3 -7.5%);
 //   kShapeLong   16-lane rows in 256-thread workgroups held at 5 waves/SIMD.
@@ -1368,17 +1369,19 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
-    const uint32_t g8 = (n + 7u) / 8u, g1 = (n + 3u) / 4u, g4 = (n + 15u) / 16u;
+    const uint32_t g8 = (n + 7u) / 8u, g4 = (n + 15u) / 16u;
 #define NFCS_ROWS(OCC, BS, G, SF)                                                                  \
     launch_rows<6, 16, OCC, BS, false, SF, BS == kBlock ? 1 : 0, BS == kBlock ? 7 : 6>(                          \
         G, BS == kBlock ? kRowsLdsPad : 0u, stream, arena, arena_bytes, desc,                                 \
                                            n, base16, status, patch, ws, nofwd)
 #define NFCS_ROWS8(SF) \
     launch_rows<6, 8, 8, 64, false, SF>(g8, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd)
+#define NFCS_SHORT(SF) \
+    launch_rows<6, 16, 7, kBlock, false, SF, 0, 6>(g4, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd)
 #define NFCS_SHAPED(SF)                                                                            \
     do {                                                                                           \
         if (shape == kShapeTiny) NFCS_ROWS8(SF);                                                   \
-        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);                                   \
+        else if (shape == kShapeShort) NFCS_SHORT(SF);                                             \
         else NFCS_ROWS(1, kBlock, g4, SF);                                                         \
     } while (0)
     if (form == kUpdateRecords) {
@@ -1398,6 +1401,7 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
                            arena, desc, n, base16, patch ? patch : ws);
     }
 #undef NFCS_SHAPED
+#undef NFCS_SHORT
 #undef NFCS_ROWS8
 #undef NFCS_ROWS
     return hipGetLastError();
@@ -1411,10 +1415,12 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
     if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
-    // The short shape's one-wave workgroups at 7 waves/SIMD: short frames make short-lived waves,
-    // and single-wave workgroups retire and relaunch them with less granularity loss (C3 +2-3%);
-    // __launch_bounds__ 7 caps the kernel at 94 SGPRs (at the compiler's 106 the SGPR file admits
-    // only 6 waves/SIMD: C3 +2%). 256-thread workgroups are held at 5 waves/SIMD by kRowsLdsPad
+    // The short shape at 7 waves/SIMD: __launch_bounds__ 7 caps the kernel at 94 SGPRs (at the
+    // compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). Its workgroups were one wave
+    // (round 3, a replayed batch: short-lived waves retire and relaunch with less granularity loss,
+    // C3 +2-3%); in the steady state 256-thread workgroups, whose 4 waves on one CU share the
+    // descriptor line of their 16 packets, measured 0.3-0.5% faster (round 5, C3 0.662-0.663
+    // against 0.665 ms per call; profiles/r05_c3_rows_ab.jsonl). 256-thread workgroups are held at 5 waves/SIMD by kRowsLdsPad
     // bytes of (unused) LDS: at the 8 their 54 VGPRs allow, the read stream runs slower (round 1,
     // one replayed batch: C1 0.768 vs 0.777 at 6). Round 4, calls rotating over fresh batches with
     // 512K-packet sub-batches: 5 waves beat 6 by 1.2-1.5% on C1, 1.6% on the C4 shard, 0.3% on C2
