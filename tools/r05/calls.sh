@@ -302,4 +302,11 @@ call_ad() {
   ab_lines gpurun_out/r5ad 3 "cur c3_wg256" "c3 --config 3 --steps 40"
 }
 
+call_ae() {
+  # round 5, GPU call ae: the forward's short-mix rows in 256-thread workgroups (fwd_wg256), the
+  # forward on the C3 mix under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ae && \
+  ab_lines gpurun_out/r5ae 3 "cur fwd_wg256" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
+
 "call_$1"

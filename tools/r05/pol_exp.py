@@ -92,6 +92,9 @@ EDITS = {
                  ("row_process<K, R, FWD, !FWD && R == 16 && BS == 64,", "row_process<K, R, FWD, !FWD && R == 16 && (BS == 64 || !LA),"),
                  ("        else if (shape == kShapeShort) NFCS_ROWS(7, 64, g1, SF);",
                   "        else if (shape == kShapeShort) launch_rows<6, 16, 7, kBlock, false, SF, 0, 6>(g4, 0u, stream, arena, arena_bytes, desc, n, base16, status, patch, ws, nofwd);")],
+    # the forward's short-mix rows in 256-thread workgroups (call ae)
+    "fwd_wg256": [("launch_rows<12, 8, 6, 64, true, SF_INLINE, 1, 12>((n + 7u) / 8u,",
+                   "launch_rows<12, 8, 6, kBlock, true, SF_INLINE, 1, 12>((n + 31u) / 32u,")],
 }
 
 for name in sys.argv[1:] or EDITS:
