@@ -309,4 +309,10 @@ call_ae() {
   ab_lines gpurun_out/r5ae 3 "cur fwd_wg256" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
 
+call_af() {
+  # round 5, GPU call af: call ae again with 6 alternating rounds (its 3 rounds fell in two modes)
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5af && \
+  ab_lines gpurun_out/r5af 6 "cur fwd_wg256" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
+
 "call_$1"
