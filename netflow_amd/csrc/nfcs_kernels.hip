@@ -1466,8 +1466,10 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
         // VGPRs). The forward's header work (decision, MAC pick, segment) then serves 8 packets per
         // instruction instead of 4; its short waves are latency-bound and every instruction is on
         // their path: C3 mix 0.519 -> 0.587 (round 3, profiles/r03_s1_ab_fwd_c3_rows.jsonl). The plain
-        // update keeps 16-lane rows there (8-lane rows of 12 slots: C3 0.569 vs 0.594).
-        launch_rows<12, 8, 6, 64, true, SF_INLINE, 1, 12>((n + 7u) / 8u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
+        // update keeps 16-lane rows there (8-lane rows of 12 slots: C3 0.569 vs 0.594). 256-thread
+        // workgroups (32 packets) since round 5: in the steady state, median 0.6915 against 0.6935 ms
+        // per call over 9 alternating processes each (profiles/r05_fwd_wg256_ab.jsonl)
+        launch_rows<12, 8, 6, kBlock, true, SF_INLINE, 1, 12>((n + 31u) / 32u, 0u, stream, arena, arena_bytes, desc, n, 0u, status,
                                                    nullptr, nullptr, fa);
         return hipGetLastError();
     }
