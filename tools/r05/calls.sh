@@ -315,4 +315,18 @@ call_af() {
   ab_lines gpurun_out/r5af 6 "cur fwd_wg256" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
 
+call_ag() {
+  # round 5, GPU call ag: rocprofv3 kernel stats of the lines whose kernels changed after call
+  # r5final3 (the short shape's and the forward short-mix's 256-thread workgroups): C3, the forward
+  # on the C3 mix, and the default line without its child lines
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ag && \
+  for spec in "c3 --config 3 --steps 30 --no-cpu --no-replay --no-host --no-c4" \
+              "l3fwd_c3 --op l3fwd --config 3 --steps 20 --no-cpu" \
+              "default --steps 20 --warmup 5 --no-cpu --no-ops"; do
+    read -r name args <<< "$spec"
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/r5ag/$name" -o $name -- \
+      python3 bench.py $args > gpurun_out/r5ag/$name.json 2> gpurun_out/r5ag/$name.err || return 1
+  done
+}
+
 "call_$1"
