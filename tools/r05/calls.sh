@@ -329,4 +329,12 @@ call_ag() {
   done
 }
 
+call_ah() {
+  # round 5, GPU call ah: the long shape's continuation batches double-buffered (libdb: batch j+1's
+  # loads issued before batch j is summed; 82 VGPRs, still 5 waves/SIMD) against the product before
+  # (libpre_db); C2 (jumbo frames: 6 batches each), C1 and the C4 shard, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ah && \
+  ab_lines gpurun_out/r5ah 3 "pre_db db" "c2 --config 2 --steps 20" "c1 --steps 50" "c4shard --packets 4194304 --steps 12"
+}
+
 "call_$1"
