@@ -337,4 +337,12 @@ call_ah() {
   ab_lines gpurun_out/r5ah 3 "pre_db db" "c2 --config 2 --steps 20" "c1 --steps 50" "c4shard --packets 4194304 --steps 12"
 }
 
+call_ai() {
+  # round 5, GPU call ai: the tiny shapes in 256-thread workgroups (tiny_wg256), 1M x 64-byte frames,
+  # the update and the forward, under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5ai && \
+  ab_lines gpurun_out/r5ai 3 "cur tiny_wg256" "tiny --config 0 --packets 1048576 --steps 40" \
+    "fwdtiny --op l3fwd --config 0 --packets 1048576 --steps 40"
+}
+
 "call_$1"

@@ -95,6 +95,11 @@ EDITS = {
     # the forward's short-mix rows in 256-thread workgroups (call ae)
     "fwd_wg256": [("launch_rows<12, 8, 6, 64, true, SF_INLINE, 1, 12>((n + 7u) / 8u,",
                    "launch_rows<12, 8, 6, kBlock, true, SF_INLINE, 1, 12>((n + 31u) / 32u,")],
+    # the tiny shapes (8-lane rows of 6 slots, 8 packets per wave) in 256-thread workgroups (call ai)
+    "tiny_wg256": [("    launch_rows<6, 8, 8, 64, false, SF>(g8, 0u, stream,",
+                    "    launch_rows<6, 8, 8, kBlock, false, SF>((n + 31u) / 32u, 0u, stream,"),
+                   ("        launch_rows<6, 8, 8, 64, true, SF_INLINE>((n + 7u) / 8u,",
+                    "        launch_rows<6, 8, 8, kBlock, true, SF_INLINE>((n + 31u) / 32u,")],
 }
 
 for name in sys.argv[1:] or EDITS:
