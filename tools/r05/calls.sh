@@ -345,4 +345,13 @@ call_ai() {
     "fwdtiny --op l3fwd --config 0 --packets 1048576 --steps 40"
 }
 
+call_aj() {
+  # round 5, GPU call aj: the forward's write pass (apply_fwd_kernel) with 2-byte stores write-through
+  # (fwdwp_wt) or plain (fwdwp_plain) instead of past the caches; the forward on C1 and on 4M frames
+  # (both deferred), 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5aj && \
+  ab_lines gpurun_out/r5aj 3 "cur fwdwp_wt fwdwp_plain" "fwdc1 --op l3fwd --steps 40" \
+    "fwd4m --op l3fwd --packets 4194304 --steps 12"
+}
+
 "call_$1"

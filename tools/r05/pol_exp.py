@@ -100,6 +100,12 @@ EDITS = {
                     "    launch_rows<6, 8, 8, kBlock, false, SF>((n + 31u) / 32u, 0u, stream,"),
                    ("        launch_rows<6, 8, 8, 64, true, SF_INLINE>((n + 7u) / 8u,",
                     "        launch_rows<6, 8, 8, kBlock, true, SF_INLINE>((n + 31u) / 32u,")],
+    # the forward's write pass (apply_fwd_kernel) stores write-through (sc1) / plain instead of past
+    # the caches (call aj)
+    "fwdwp_wt": [('    asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");',
+                  '    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");')],
+    "fwdwp_plain": [('    asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");',
+                     '    asm volatile("global_store_short %0, %1, off" ::"v"(p), "v"(v) : "memory");')],
 }
 
 for name in sys.argv[1:] or EDITS:
