@@ -72,6 +72,24 @@ def test_host_path_argument_rules(engine):
     assert np.array_equal(arena, before)
 
 
+@pytest.mark.parametrize("n", [1, 70_000])
+def test_scattered_frame_larger_than_a_slot_is_rejected_untouched(engine, n):
+    """nfcs_update_host_frames checks every frame against the 64 MiB staging slot before anything is
+    staged (over the copy threads from 65,536 frames on): one frame claiming 64 MiB + 1 bytes makes
+    the call NFCS_EINVAL, and no frame is read or written (the frames here are 64-byte runts of one
+    small buffer; the oversized one points at it too)."""
+    L = nf.lib()
+    buf = np.random.default_rng(n).integers(0, 256, 64 * 16, dtype=np.uint8)
+    before = buf.copy()
+    ptrs = (buf.ctypes.data + (np.arange(n, dtype=np.uint64) % 16) * 64).astype(np.uint64)
+    lens = np.full(n, 64, dtype=np.uint32)
+    lens[n // 2] = (64 << 20) + 1
+    status = np.full(n, 0xAB, dtype=np.uint8)
+    assert L.nfcs_update_host_frames(engine.ctx, ptrs.ctypes.data, lens.ctypes.data, n, status.ctypes.data, 0) == EINVAL
+    assert np.array_equal(buf, before)
+    assert (status == 0xAB).all()
+
+
 def test_host_path_takes_descriptors_in_any_order(engine):
     """Round 5: nfcs_update_host no longer requires arena order — descriptors
     in reverse order (every frame its own run of ascending offsets) give the oracle's bytes and
