@@ -354,4 +354,11 @@ call_aj() {
     "fwd4m --op l3fwd --packets 4194304 --steps 12"
 }
 
+call_al() {
+  # round 5, GPU call al: the short shape's inline byte stores with `nt` alone (c3_st_nt) / `sc1 nt`
+  # (c3_st_sc1nt) instead of `sc0 sc1 nt`; C3 under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5al && \
+  ab_lines gpurun_out/r5al 3 "cur c3_st_nt c3_st_sc1nt" "c3 --config 3 --steps 40"
+}
+
 "call_$1"

@@ -106,6 +106,12 @@ EDITS = {
                   '    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");')],
     "fwdwp_plain": [('    asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");',
                      '    asm volatile("global_store_short %0, %1, off" ::"v"(p), "v"(v) : "memory");')],
+    # the short shape's inline byte stores with `nt` alone / `sc1 nt` instead of `sc0 sc1 nt` (call al;
+    # st8_nt's other users, the forward's odd TCP offsets and VLAN's tails, see the same change)
+    "c3_st_nt": [('    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes',
+                  '    asm volatile("global_store_byte %0, %1, off nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes')],
+    "c3_st_sc1nt": [('    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes',
+                     '    asm volatile("global_store_byte %0, %1, off sc1 nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes')],
 }
 
 for name in sys.argv[1:] or EDITS:
