@@ -361,4 +361,12 @@ call_al() {
   ab_lines gpurun_out/r5al 3 "cur c3_st_nt c3_st_sc1nt" "c3 --config 3 --steps 40"
 }
 
+call_an() {
+  # round 5, GPU call an: the forward's deferred long-frame read pass with line-aligned windows in
+  # every wave (fwd_lam1; round 3 measured it 1.3% slower on replayed 128-byte starts); the forward
+  # on C1 and 4M frames under rotation, 3 alternating rounds
+  cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r5an && \
+  ab_lines gpurun_out/r5an 3 "cur fwd_lam1" "fwdc1 --op l3fwd --steps 40" "fwd4m --op l3fwd --packets 4194304 --steps 12"
+}
+
 "call_$1"

@@ -112,6 +112,9 @@ EDITS = {
                   '    asm volatile("global_store_byte %0, %1, off nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes')],
     "c3_st_sc1nt": [('    asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes',
                      '    asm volatile("global_store_byte %0, %1, off sc1 nt" ::"v"(p), "v"(b) : "memory");\n}\n// The same for 16 bytes')],
+    # the forward's long-frame read pass with line-aligned windows in every wave (LAM 1, as the
+    # update's long shape) instead of per wave (LAM 2) (call an)
+    "fwd_lam1": [("launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 2, 7>", "launch_rows<6, 16, 7, kBlock, true, SF_DEFER, 1, 7>")],
 }
 
 for name in sys.argv[1:] or EDITS:
