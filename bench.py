@@ -922,6 +922,10 @@ def mix_line(eng, args, op: str):
         ctr[0] += 1
         call(a, b, d)
     steps = max(args.steps // 2, 10)
+    if op == "l3fwd":
+        # each of the 2 batches is forwarded steps / 2 times per timed region: TTL 64 allows 63
+        # (an uncapped --steps ran the timed region over expired, unwritten packets)
+        steps = min(steps, 2 * 63)
     tw, done = time.perf_counter(), 0
     while done < args.warmup or time.perf_counter() - tw < 0.3:
         step()

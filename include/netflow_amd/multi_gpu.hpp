@@ -47,7 +47,8 @@ public:
     size_t size() const { return ctx_.size(); }
     nfcs_ctx* context(size_t i) const { return ctx_[i]; }
 
-    // nfcs_update_host over the contexts: descriptors in arena order, as nfcs_update_host requires;
+    // nfcs_update_host over the contexts: descriptors in any order (ABI 2: each context stages its
+    // range's runs of ascending offsets as spans, so a range in arena order stages as one span);
     // status (optional) receives every packet's NFCS_ST_* byte at its own index. bounds (optional,
     // size() + 1 entries) receives the ranges used: context p took packets [bounds[p], bounds[p+1]).
     // Returns NFCS_OK or the first negative error of any range (every range has finished by then).

@@ -341,17 +341,16 @@ int ChecksumEngine::update_checksums_batch(Pkt* const* pkts, size_t n, uint8_t* 
     // then the transfers, then one scatter, one after the other)
     frames_.resize(n);
     lens_.resize(n);
-    std::atomic<bool> too_long{false};
+    // a data window longer than NFCS_FRAME_RELEVANT_BYTES goes as its first NFCS_FRAME_RELEVANT_BYTES
+    // bytes: update_checksums() gives the same result (nfcs.h), so no PacketBuffer size is refused
     detail::parallel_ranges(n, [&](size_t i0, size_t i1) {
         for (size_t i = i0; i < i1; ++i) {
             auto* b = pkts[i] ? pkts[i]->get_buffer() : nullptr;
             const size_t len = b ? b->get_data_length() : 0;
-            if (len > 0xFFFFFFFFu) too_long.store(true, std::memory_order_relaxed);
             frames_[i] = b ? b->get_data_start_ptr() : nullptr;
-            lens_[i] = static_cast<uint32_t>(len);
+            lens_[i] = static_cast<uint32_t>(std::min<size_t>(len, NFCS_FRAME_RELEVANT_BYTES));
         }
     });
-    if (too_long.load()) return NFCS_EINVAL;
     return nfcs_update_host_frames(ctx_, frames_.data(), lens_.data(), static_cast<uint32_t>(n), status, 0);
 }
 
@@ -673,8 +672,11 @@ inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uin
     }
     // nfcs_update_host stages each run of ascending offsets as one span: a burst in allocation order
     // (the pool hands slots out in arena order) or wrapping once goes as it is; a burst in an order
-    // the pool's reuse has scrambled is sorted first, so its spans stay long
-    if (drops <= 1) {
+    // the pool's reuse has scrambled is sorted first, so its spans stay long. A wrap is one drop whose
+    // second run ends at or before the first run's first frame ([100..199, 0, 9000] also
+    // has one drop, but staged as is its second span would carry every slot from 0 to 9000)
+    const bool wrap = drops == 1 && (uint64_t)desc[n - 1].off16 * 16 + desc[n - 1].len <= (uint64_t)desc[0].off16 * 16;
+    if (drops == 0 || wrap) {
         return eng_.update_host(arena_, slots_ * slot_bytes_, desc.data(), static_cast<uint32_t>(n), status, flags);
     }
     std::vector<uint32_t> order(n);

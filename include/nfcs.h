@@ -35,7 +35,10 @@ extern "C" {
 #define NFCS_API
 #endif
 
-#define NFCS_ABI_VERSION 1
+/* ABI versions: 1 = rounds 1-4; 2 = round 5 on: nfcs_update_host_frames, and nfcs_update_host accepts
+ * descriptors in any order (an ABI-1 library returns NFCS_EINVAL for a burst that is not one ascending
+ * run). A caller that needs either checks nfcs_abi_version() >= 2. */
+#define NFCS_ABI_VERSION 2
 
 /* ---- data layout ------------------------------------------------------------------ */
 
@@ -168,7 +171,7 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
 
 /* Same on host memory (NIC / socket buffers). Synchronous. Descriptors may come in any order;
  * each run of ascending offsets is staged as a contiguous span (a NIC ring burst that wraps past
- * the ring's end is two runs; ABI 1 before round 5 required one ascending run). Frames go H2D in
+ * the ring's end is two runs; ABI 1 required one ascending run). Frames go H2D in
  * chunks on two streams (from a pageable arena through the context's pinned ring, copied by host
  * threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs per
  * chunk, and only the 8-byte nfcs_patch records come back and are applied on the host. A frame
@@ -199,10 +202,14 @@ NFCS_API int nfcs_update_host(nfcs_ctx* ctx, uint8_t* h_arena, uint64_t arena_by
  * checksum bytes written back into each frame in place (ip field first, then l4, the reference's
  * write order); the gather, the transfers, the kernel and the write-back of successive chunks
  * overlap on two streams. Only the bytes the reference writes are written. frames[i] == NULL or
- * lens[i] == 0: nothing read or written, status NFCS_ST_NONE. A frame longer than one staging
- * slot (64 MiB) is NFCS_EINVAL, checked before anything is queued. Frames must not overlap.
+ * lens[i] == 0: nothing read or written, status NFCS_ST_NONE. A frame longer than
+ * NFCS_FRAME_RELEVANT_BYTES is processed as its first NFCS_FRAME_RELEVANT_BYTES bytes, with the same
+ * result: update_checksums() reads, and compares with data_len, no offset past 65,613 (l2 18 + IHL 60
+ * + a 16-bit length; packet.hpp:728-889), so any longer length passes each of its bounds tests alike
+ * (ABI 2 as first shipped returned NFCS_EINVAL above 64 MiB). Frames must not overlap.
  *   h_status  optional (NULL) n status bytes, NFCS_ST_*
  *   flags     0 (reserved) */
+#define NFCS_FRAME_RELEVANT_BYTES 131072u
 NFCS_API int nfcs_update_host_frames(nfcs_ctx* ctx, uint8_t* const* frames, const uint32_t* lens, uint32_t n,
                                      uint8_t* h_status, uint32_t flags);
 

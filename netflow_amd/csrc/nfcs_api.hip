@@ -956,11 +956,13 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
     if (!frames || !lens || flags != 0) return NFCS_EINVAL;
     int rc = ensure_host_pipeline(c);
     if (rc) return rc;
-    auto flen = [&](uint32_t i) -> uint64_t { return frames[i] ? lens[i] : 0u; };  // a NULL frame is empty
+    // a NULL frame is empty; a frame longer than kFrameRelevantBytes is staged as its first
+    // kFrameRelevantBytes bytes, which changes nothing (nfcs.h): so no frame outgrows a staging slot
+    auto flen = [&](uint32_t i) -> uint64_t { return frames[i] ? std::min(lens[i], nfcs::kFrameRelevantBytes) : 0u; };
     auto pad = [](uint64_t len) { return (len + 15u) & ~15ull; };
     const int parts = c->workers.size() + 1;
-    // every frame fits one staging slot (checked before anything is queued) and the burst's padded
-    // bytes, over the workers for large bursts (no serial pass over the burst on the caller's thread)
+    // the burst's padded bytes (every frame fits one staging slot: checked anyway), over the workers
+    // for large bursts (no serial pass over the burst on the caller's thread)
     uint64_t chunk_target = 0;
     {
         constexpr int kMaxParts = 65;

@@ -43,6 +43,8 @@ constexpr uint32_t kDeferMeanBytes = 1280;
 // jumbo frames 5% slower; 128K C1 even). The packet count alone decides: the arena size never
 // changes the form.
 constexpr uint32_t kInlineMaxPackets = 65536;
+// update_checksums() reads and tests against data_len no offset past 65,613 (nfcs.h)
+constexpr uint32_t kFrameRelevantBytes = NFCS_FRAME_RELEVANT_BYTES;
 // kUpdateAuto on long frames processes a batch of more than kSubBatchAbovePackets as sub-batches
 // of kSubBatchPackets (read pass, then write pass, per sub-batch): 512K header lines (64 MB,
 // 128 MB when frames straddle lines) stay in the 256 MB memory-side cache between the two passes.

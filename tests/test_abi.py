@@ -44,7 +44,7 @@ def test_library_contains_gfx950_code_object():
 
 
 def test_error_conventions_without_gpu(lib):
-    assert lib.nfcs_abi_version() == 1
+    assert lib.nfcs_abi_version() == 2
     assert lib.nfcs_strerror(0) == b"ok"
     assert lib.nfcs_strerror(-1) == b"invalid argument"
     # null context / arguments are rejected, never crash

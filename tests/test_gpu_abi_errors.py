@@ -126,7 +126,7 @@ def test_strerror_covers_every_code():
     for rc in (0, -1, -2, -3, -4):
         msg = L.nfcs_strerror(rc)
         assert isinstance(msg, bytes) and len(msg) > 0
-    assert L.nfcs_abi_version() == 1
+    assert L.nfcs_abi_version() == 2
     assert isinstance(ctypes.c_int(L.nfcs_last_hip_error()).value, int)
 
 

@@ -193,7 +193,7 @@ def test_update_waves_at_the_wave_buffer_span_boundary(engine, big, delta16):
     d_desc = engine.alloc(desc.nbytes).upload(desc)
     d_st = engine.alloc(n)
     try:
-        engine.set_slot_bytes(900)  # the short shape (16-lane rows, one-wave workgroups, buffer loads)
+        engine.set_slot_bytes(900)  # the short shape (16-lane rows in 256-thread workgroups, frame-relative windows, buffer loads)
         engine.update_device(big, b0 + region_b.nbytes, d_desc, n, d_st)
         engine.sync()
         assert np.array_equal(d_st.download(np.uint8, n), rst)

@@ -191,6 +191,23 @@ def test_scattered_small_bursts(engine):
     assert (st == nf.ST_NONE).all() and np.array_equal(buf, before)
 
 
+def test_scattered_frames_longer_than_a_staging_slot(engine):
+    """Data windows longer than NFCS_FRAME_RELEVANT_BYTES (128 KiB) — one of them longer than a 64 MiB
+    staging slot, which round 5's ABI 2 refused with NFCS_EINVAL — go as their first
+    128 KiB: the reference reads and bounds-tests no offset past 65,613, so bytes and statuses equal
+    the oracle's on the whole frames, and nothing past the checksum fields changes."""
+    base = oracle.fuzz_frames(46, 0, 64)
+    rng = np.random.default_rng(13)
+    sizes = [0, 200_000, (64 << 20) + 4096, 131_071, 131_072, 131_073]
+    frames = [f + rng.integers(0, 256, max(0, sz - len(f)), dtype=np.uint8).tobytes() if sz else f
+              for f, sz in zip(base, sizes * 11)]
+    buf, offs, lens = scattered(frames, 14)
+    want, wst = expected(buf, offs, lens)
+    st = engine.update_host_frames(buf, offs, lens)
+    assert np.array_equal(st, wst)
+    assert np.array_equal(buf, want)
+
+
 @pytest.mark.parametrize("mode", ["patch", "frames"])
 @pytest.mark.parametrize("shift", [1, 8, 13])
 def test_pageable_arena_at_any_address(engine, mode, shift):
