@@ -414,6 +414,9 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--align", type=int, default=128,
                     help="frame start alignment in the arena: 128 = one L2 line per frame start, as "
                          "NIC/DPDK buffer rings lay frames out (16 = densely packed)")
+    ap.add_argument("--slot-bytes", type=int, default=0,
+                    help="the context's slot-size hint (nfcs_ctx_set_slot_bytes; speed only): 0 = the "
+                         "launch shape follows the batch's mean footprint")
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="minimum untimed warm-up time (on top of --warmup steps)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -477,6 +480,8 @@ def main():
     if not torch_device_init(dev):
         raise SystemExit("bench.py: torch sees no GPU (needs a ROCm GPU for torch.cuda.synchronize)")
     eng = nf.Engine(dev)
+    if args.slot_bytes:
+        eng.set_slot_bytes(args.slot_bytes)
     d_arena, nbytes, d_desc, hdesc = eng.config_batch(args.config, SEED, first, n, args.align)
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     algo_bytes = frame_bytes + 12.0 * n  # + 2x2 B checksum writes + 8 B descriptor per packet
@@ -767,6 +772,8 @@ def main():
         out["c4_shard"] = c4_shard_line(eng, args)
         if not args.no_mix:
             out["c3"] = mix_line(eng, args, "update")
+            # SURVEY §8d's own layout, frames packed at 16-byte starts
+            out["c3_packed"] = mix_line(eng, args, "update", 16)
             out["l3fwd_c3"] = mix_line(eng, args, "l3fwd")
         if not args.no_host:
             out["host"] = host_line(eng, args, n)
@@ -880,17 +887,19 @@ def c4_shard_line(eng, args):
             "parity": {"digest": got, "reference_digest": want, "match": None if want is None else got == want}}
 
 
-def mix_line(eng, args, op: str):
+def mix_line(eng, args, op: str, align: int = 0):
     """BASELINE C3 — 4M x U{64..1500} B IPv4 TCP/UDP, the length-divergence stress and the lines
     furthest below roofline — as a sub-line of the N = 1 line, so the driver's clock covers it
     (VERDICT r4 item 1): `op` "update" (nfcs_update_device, the short shape) or "l3fwd" (the fused
     forward, switch.hpp:279-294, next hop i % 9, its short-mix shape). Calls rotate over 2 separately
     generated batches (the steady state), warm-up, wall clock over the steps, HIP events on the
     engine's stream around the rotated calls, the reference's digest of the result (configs.json
-    configs[3] / l3fwd_more) for both batches."""
+    configs[3] / l3fwd_more) for both batches. `align` (default --align): the frame starts; 16 packs
+    the frames densely, SURVEY §8d's arena layout (the `c3_packed` sub-line)."""
     n = DEFAULT_PACKETS[3]
-    d_arena, nbytes, d_desc, hdesc = eng.config_batch(3, SEED, 0, n, args.align)
-    batches = [(d_arena, nbytes, d_desc), eng.config_batch(3, SEED, 0, n, args.align)[:3]]
+    align = align or args.align
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(3, SEED, 0, n, align)
+    batches = [(d_arena, nbytes, d_desc), eng.config_batch(3, SEED, 0, n, align)[:3]]
     frame_bytes = float(hdesc["len"].astype(np.float64).sum())
     ctr = [0]
     extra = []
@@ -955,7 +964,7 @@ def mix_line(eng, args, op: str):
     achieved = algo_bytes / (ev_ms * 1e-3) / 1e9
     return {"workload": "C3: 4M x U{64..1500} B IPv4 TCP/UDP mix, device-resident"
                         + (", fused L3 forward (next hop i % 9)" if op == "l3fwd" else ""),
-            "packets": n, "steps": steps, "batches_rotated": 2, "value": round(frame_bytes / dt / 1e9, 2),
+            "frame_align": align, "packets": n, "steps": steps, "batches_rotated": 2, "value": round(frame_bytes / dt / 1e9, 2),
             "unit": "GB/s", "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ev_ms, 4),
             "algorithmic_bytes_per_launch": int(algo_bytes),
             "frac": round(achieved / HBM_PEAK_GBS, 4),

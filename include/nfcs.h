@@ -132,10 +132,12 @@ NFCS_API void* nfcs_ctx_stream(nfcs_ctx* ctx); /* the context's own hipStream_t 
 /* Launch shapes (speed only; the bytes written never depend on them) follow the mean footprint per
  * packet: 8-lane rows for short frames, 16-lane rows for long ones, long-frame sub-batches. Without
  * a hint it is arena_bytes / n, which is exact for a batch that fills its arena and otherwise only
- * over-estimates; when that estimate says "long", the update and the L3 forward also sample the
- * frames' real footprint on the device (256 descriptors, one wave, no host sync), and the next call
- * over the same burst (descriptor array, n and arena_bytes) launches in the shape the sample calls for — a burst inside a larger
- * ring (a NIC ring reusing its descriptor array) adapts after one call. A caller may
+ * over-estimates; when that estimate says "long" or "8-lane rows", the update, the L3 forward and
+ * VLAN also sample the frames on the device (256 descriptors, one wave, no host sync: the mean of their
+ * lengths rounded up to 128 and how many exceed one 8-lane row pass), and the next call over the same
+ * burst (descriptor array, n and arena_bytes) launches in the shape the sample calls for — a burst
+ * inside a larger ring (a NIC ring reusing its descriptor array) adapts after one call,
+ * and so does a densely packed mix of short and long frames (§5e). A caller may
  * instead state its frames' mean slot size, e.g. 128 for 64-byte frames in 128-byte slots; 0 (the
  * default) restores the automatic choice. Applies to the device-path calls that follow on ctx
  * (update, L3 forward, VLAN; nfcs_update_host measures each staged chunk itself). */

@@ -559,25 +559,33 @@ int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
 }
 // The shape a call over this burst launches in, without side effects (nfcs_ctx_launch_footprint):
 // *slot = the burst's observation slot, -1 when it has none yet (the call then takes one).
+// Estimates that a sample can correct: "long" (a burst inside a larger ring), and "8-lane rows" (a
+// densely packed mix whose frames often need a second 8-lane row pass; round 6).
+bool sampled_estimate(uint64_t est) { return est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes; }
 Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot) {
     *slot = -1;
     if (c->slot_bytes) return {c->slot_bytes, {}};
     if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
     const uint64_t est = arena_bytes / n;
-    if (est < nfcs::kSmallMeanBytes || !c->obs_host) return {est, {}};
+    if (!sampled_estimate(est) || !c->obs_host) return {est, {}};
     const int k = find_burst(c, arena_bytes, d_desc, n);
     if (k < 0) return {est, {}};
     *slot = k;
     // the latest sample of this burst's generation (a late one of an earlier burst has another)
     const uint64_t o = __atomic_load_n(c->obs_host + k, __ATOMIC_RELAXED);
     const uint32_t gen = c->obs_burst[k].gen;
-    const uint64_t mean = (uint32_t)(o >> 32) == gen ? (uint32_t)o : 0;
-    return {mean ? std::min<uint64_t>(mean, est) : est, {c->obs_dev + k, ((uint64_t)gen << 32) | n}};
+    const nfcs::ObsReq req = {c->obs_dev + k, ((uint64_t)gen << 32) | n};
+    if ((uint32_t)(o >> 32) != gen || !((uint32_t)o & nfcs::kObsPresent)) return {est, req};
+    uint64_t mean = std::min<uint64_t>((uint32_t)o & nfcs::kObsMeanMask, est);
+    // 8-lane rows only for frames that mostly fit their one row pass (nfcs_internal.h kTinyLongMax)
+    if (mean < nfcs::kTinyMeanBytes && (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
+        mean = nfcs::kTinyMeanBytes;
+    return {mean, req};
 }
 Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
     int k = -1;
     Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k);
-    if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && arena_bytes / n >= nfcs::kSmallMeanBytes) {
+    if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && sampled_estimate(arena_bytes / n)) {
         // a burst not seen lately: the least recently used slot, under a new generation
         k = 0;
         for (int j = 1; j < nfcs_ctx::kObsSlots; ++j)

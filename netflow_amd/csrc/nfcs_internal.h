@@ -70,6 +70,21 @@ constexpr uint64_t kSmallMeanBytes = 1200;
 // uniform 64-256 B frames 1.8-1.9x, IMIX 7:4:1 of 64/570/1500 B 1.47x, 768 B 1.2x; the C3 mix,
 // 870 B of footprint per packet, stays on 16-lane rows, where 8-lane rows lose 7.5%).
 constexpr uint64_t kTinyMeanBytes = 800;
+// One row pass of those 8-lane rows (6 slots of 8 x 16 bytes); a wave with a longer frame makes a
+// second one. So a mix whose mean alone says 8-lane rows but whose frames often exceed this (C3's
+// U{64..1500} packed at 16-byte starts: 782 B of footprint, half the frames longer) runs 16-lane rows
+// once its footprint sample (sample_footprint) finds more than kTinyLongMax of 256 sampled frames
+// longer than this: round 6, packed C3 0.787-0.818 ms per call in 8-lane rows against 0.655 in the
+// 16-lane short shape (profiles/r06_c3_packed_shapes.jsonl). A wave of 8 frames of which a fraction
+// p is long continues with probability 1 - (1 - p)^8; with a continued 8-lane wave costing about
+// 1.2x two 16-lane waves (the packed C3 figures) and an uncontinued one 0.6x, they break even near
+// p = 1/8 (32 of 256): IMIX 7:4:1 (64/570/1500 B, p = 1/12) stays on 8-lane rows.
+constexpr uint32_t kTinyRowBytes = 768;
+constexpr uint32_t kTinyLongMax = 32;
+// The footprint sample's 32-bit word (sample_footprint; the burst's generation in the other 32 bits).
+constexpr uint32_t kObsPresent = 0x80000000u;
+constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)
+constexpr uint32_t kObsMeanMask = 0xFFFFFu;  // bits 0-19: the mean of the lengths rounded up to 128
 // VLAN push/pop below this mean footprint writes its frames write-through (`sc1`), at or above it
 // past the caches (`sc0 sc1 nt`): 1M frames in 128-byte slots 177 vs 181 µs, in 384 / 640-byte
 // slots 212-216 vs 208 / 258 vs 245 µs, C1 0.698-0.704 vs 0.728-0.731.

@@ -694,27 +694,33 @@ struct FwdArgs {
     ObsReq obs;
 };
 
-// The mean footprint of a call's frames — 256 descriptors spread evenly over the call's tag & 0xFFFFFFFF
-// packets from desc (the whole call, also when it runs as sub-batches: the first sub-batch samples),
-// each length rounded up to 128 bytes — written to *obs (host-mapped, system scope) by one wave of the
+// The footprint of a call's frames — 256 descriptors spread evenly over the call's tag & 0xFFFFFFFF
+// packets from desc (the whole call, also when it runs as sub-batches: the first sub-batch samples):
+// the mean of their lengths rounded up to 128 bytes, and how many of the 256 are longer than one
+// 8-lane row pass (kTinyRowBytes) — written to *obs (host-mapped, system scope) by one wave of the
 // launch, in one 64-bit store together with the burst's generation (tag >> 32), so the host can tell
-// a late sample of an earlier burst from this one's. The next call over the same burst (descriptor
-// array, n and arena_bytes) picks its launch shape from it when arena_bytes / n cannot tell (a burst
-// inside a larger ring; nfcs_api.hip launch_shape). Speed only.
+// a late sample of an earlier burst from this one's: kObsPresent | longs << kObsLongShift | mean. The
+// next call over the same burst (descriptor array, n and arena_bytes) picks its launch shape from it
+// when arena_bytes / n cannot tell (a burst inside a larger ring; a densely packed mix whose mean
+// alone says 8-lane rows; nfcs_api.hip launch_shape). Speed only.
 DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint32_t lane, uint64_t* obs) {
     const uint32_t n = (uint32_t)tag;
-    uint32_t s = 0;
+    uint32_t s = 0, c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         const uint32_t len = desc[(uint32_t)(((uint64_t)(4u * lane + k) * n) >> 8)].len;
         s += ((len < 0xFFFFu ? len : 0xFFFFu) + 127u) & ~127u;
+        c += len > kTinyRowBytes ? 1u : 0u;
     }
     s = row_sum<16>(s);
+    c = row_sum<16>(c);
     const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)s, 0) + (uint32_t)__builtin_amdgcn_readlane((int)s, 16) +
                        (uint32_t)__builtin_amdgcn_readlane((int)s, 32) + (uint32_t)__builtin_amdgcn_readlane((int)s, 48);
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) + (uint32_t)__builtin_amdgcn_readlane((int)c, 16) +
+                       (uint32_t)__builtin_amdgcn_readlane((int)c, 32) + (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
     if (lane == 0)
-        __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | ((t >> 8) | 1u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | kObsPresent | (l << kObsLongShift) | (t >> 8),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Issue the row's K chunk loads: the header slot with the default cache policy (its lines are

@@ -33,6 +33,7 @@
 #include <netflow++/packet.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <functional>
@@ -749,10 +750,218 @@ int adapterbench_mode(size_t n, size_t reps, size_t threads, const std::string& 
     return 0;
 }
 
+// The reference's per-packet calls spread over k threads the way a switch that splits its RX bursts
+// over cores would: workers started once, spinning on a generation counter between bursts (a thread
+// spawned per burst would cost more than a 256-packet burst's checksums).
+class SpinPool {
+public:
+    explicit SpinPool(size_t k) : k_(std::max<size_t>(1, k)) {
+        for (size_t t = 1; t < k_; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~SpinPool() {
+        quit_.store(true);
+        gen_.fetch_add(1, std::memory_order_release);
+        for (auto& x : th_) x.join();
+    }
+    // f(i0, i1) over [0, n), split into k contiguous slices; the caller runs slice 0
+    void run(size_t n, const std::function<void(size_t, size_t)>& f) {
+        f_ = &f;
+        n_ = n;
+        left_.store(k_ - 1, std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_release);
+        f(0, n / k_);
+        while (left_.load(std::memory_order_acquire)) __builtin_ia32_pause();
+    }
+
+private:
+    void loop(size_t t) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g;
+            while ((g = gen_.load(std::memory_order_acquire)) == seen) __builtin_ia32_pause();
+            seen = g;
+            if (quit_.load()) return;
+            (*f_)(n_ * t / k_, n_ * (t + 1) / k_);
+            left_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    size_t k_;
+    std::vector<std::thread> th_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<size_t> left_{0};
+    std::atomic<bool> quit_{false};
+    const std::function<void(size_t, size_t)>* f_ = nullptr;
+    size_t n_ = 0;
+};
+
+// The per-RX-burst operating point of INTEGRATION.md §2: a ring of `ring` BASELINE
+// C1 frames (1500 B IPv4+UDP, the seeded generator) checksummed burst by burst, consecutive bursts of b
+// packets walking the ring (wrapping), for every b in `sizes`, through
+//   adapter      netflow_amd::update_checksums_batch over the reference's own netflow::Packet /
+//                PacketBuffer objects (one `new[]` each; nfcs_update_host_frames: gather, H2D, GPU,
+//                checksum bytes written back);
+//   pinned_ring  nfcs_update_host over the same frames in one pinned arena, 1536-byte slots (a NIC
+//                ring's DMA area; frames H2D, patch records back);
+//   reference_1_thread / reference_threads  the reference's per-packet Packet::update_checksums() over
+//                the burst's PacketBuffers, on one thread (the switch's own loop, switch.hpp:213-294) and
+//                on `threads` threads (a SpinPool).
+// Each call is timed alone (steady clock); a leg runs for `seconds` and at least 20 calls; reported: the
+// median and 10th percentile µs per call and GB/s of frames at the median. update_checksums() is
+// idempotent, so calls over frames an earlier leg updated cost the same. Parity per path: from the
+// pristine frames, every leg, then one more pass over the whole ring, then the ring's digest against
+// `want` (the reference's digest of these frames, tests/golden/configs.json). Prints one JSON line.
+int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double seconds, size_t threads,
+                    const std::string& want) {
+    using clk = std::chrono::steady_clock;
+    int rc = NFCS_OK;
+    netflow_amd::ChecksumEngine* eng = netflow_amd::ChecksumEngine::try_instance(&rc);
+    if (!eng) {
+        std::printf("{\"error\": \"no engine: %s\"}\n", nfcs_strerror(rc));
+        return 1;
+    }
+    nfcs_ctx* c = eng->ctx();
+    const size_t n = ring;
+    std::vector<nfcs_desc> desc(n);
+    uint64_t bytes = 0;
+    if (nfcs_layout_config(NFCS_CFG_C1_1500B_UDP, 20250620ull, 0, (uint32_t)n, 128, desc.data(), &bytes)) return 1;
+    void *d_arena = nullptr, *d_desc = nullptr, *h_ring = nullptr;
+    if (nfcs_device_alloc(c, bytes, &d_arena) || nfcs_device_alloc(c, n * sizeof(nfcs_desc), &d_desc) ||
+        nfcs_host_alloc(c, bytes, &h_ring))
+        return 1;
+    if (nfcs_memcpy_h2d(c, d_desc, desc.data(), n * sizeof(nfcs_desc))) return 1;
+    if (nfcs_gen_config_device(c, NFCS_CFG_C1_1500B_UDP, 20250620ull, 0, (uint32_t)n, (uint8_t*)d_arena, bytes,
+                               (nfcs_desc*)d_desc, nullptr) || nfcs_stream_sync(c, nullptr))
+        return 1;
+    std::vector<uint8_t> pristine(bytes);
+    if (nfcs_memcpy_d2h(c, pristine.data(), d_arena, bytes)) return 1;
+    uint8_t* pr = static_cast<uint8_t*>(h_ring);
+    SpinPool copier(std::max<size_t>(1, std::min<size_t>(threads, 8)));  // restores and digests only, untimed
+
+    std::vector<std::unique_ptr<netflow::PacketBuffer>> rb(n);
+    std::vector<std::unique_ptr<netflow::Packet>> rp(n);
+    std::vector<netflow::Packet*> ptrs(n);
+    for (size_t i = 0; i < n; ++i) {
+        rb[i].reset(new netflow::PacketBuffer(kHeadroom + 1536, kHeadroom, desc[i].len));
+        rp[i].reset(new netflow::Packet(rb[i].get()));
+        ptrs[i] = rp[i].get();
+    }
+    auto frame = [&](size_t i) -> const uint8_t* { return pristine.data() + (size_t)desc[i].off16 * 16; };
+    auto restore = [&](bool ring_arena) {
+        copier.run(n, [&](size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i) {
+                uint8_t* d = ring_arena ? pr + (size_t)desc[i].off16 * 16 : rb[i]->get_data_start_ptr();
+                std::memcpy(d, frame(i), desc[i].len);
+            }
+        });
+    };
+    std::vector<uint8_t> img(bytes);
+    auto digest = [&](bool ring_arena) -> std::string {
+        if (!ring_arena)
+            copier.run(n, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i)
+                    std::memcpy(img.data() + (size_t)desc[i].off16 * 16, rb[i]->get_data_start_ptr(), desc[i].len);
+            });
+        uint64_t d = 0;
+        if (nfcs_memcpy_h2d(c, d_arena, ring_arena ? pr : img.data(), bytes) ||
+            nfcs_digest_device(c, (uint8_t*)d_arena, bytes, (nfcs_desc*)d_desc, (uint32_t)n, 0, &d, nullptr))
+            return "error";
+        char s[32];
+        std::snprintf(s, sizeof(s), "%016llx", (unsigned long long)d);
+        return s;
+    };
+    double frame_len = desc[0].len;
+
+    // one path: call(off, b) checksums packets [off, off + b) of the ring
+    std::string out;
+    bool all_match = true;
+    auto path = [&](const char* name, bool ring_arena, const std::function<int(size_t, size_t)>& call) -> int {
+        restore(ring_arena);
+        std::string legs;
+        size_t off = 0;
+        for (size_t b : sizes) {
+            if (b == 0 || n % b) return NFCS_EINVAL;
+            std::vector<double> us;
+            int r = call(off, b);  // warm: staging ring, pinned buffers, code, the workers
+            off = (off + b) % n;
+            const auto t_end = clk::now() + std::chrono::duration<double>(seconds);
+            while (r == NFCS_OK && (us.size() < 20 || clk::now() < t_end)) {
+                const auto t0 = clk::now();
+                r = call(off, b);
+                us.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+                off = (off + b) % n;
+            }
+            if (r) return r;
+            std::sort(us.begin(), us.end());
+            const double med = us[us.size() / 2], p10 = us[us.size() / 10];
+            char o[256];
+            std::snprintf(o, sizeof(o), "%s\"%zu\": {\"us_per_call\": %.2f, \"us_p10\": %.2f, \"GBps\": %.3f, \"calls\": %zu}",
+                          legs.empty() ? "" : ", ", b, med, p10, b * frame_len / (med * 1e-6) / 1e9, us.size());
+            legs += o;
+        }
+        const size_t big = sizes.back();
+        for (size_t k = 0; k < n / big; ++k) {  // one whole pass, untimed: every frame updated
+            const int r = call(k * big, big);
+            if (r) return r;
+        }
+        const std::string d = digest(ring_arena);
+        all_match = all_match && d == want;
+        char o[160];
+        std::snprintf(o, sizeof(o), "}, \"digest\": \"%s\", \"match\": %s}", d.c_str(), d == want ? "true" : "false");
+        out += std::string(out.empty() ? "" : ", ") + "\"" + name + "\": {\"bursts\": {" + legs + o;
+        return NFCS_OK;
+    };
+
+    rc = path("adapter", false, [&](size_t off, size_t b) { return netflow_amd::update_checksums_batch(ptrs.data() + off, b); });
+    if (!rc)
+        rc = path("pinned_ring", true, [&](size_t off, size_t b) {
+            return nfcs_update_host(c, pr, bytes, desc.data() + off, (uint32_t)b, nullptr, 0);
+        });
+    if (!rc)
+        rc = path("pinned_ring_zero_copy", true, [&](size_t off, size_t b) {
+            return nfcs_update_host(c, pr, bytes, desc.data() + off, (uint32_t)b, nullptr, NFCS_HOST_ZERO_COPY);
+        });
+    if (!rc)
+        rc = path("reference_1_thread", false, [&](size_t off, size_t b) {
+            for (size_t i = off; i < off + b; ++i) ptrs[i]->update_checksums();
+            return 0;
+        });
+    if (!rc) {
+        SpinPool pool(threads);
+        rc = path("reference_threads", false, [&](size_t off, size_t b) {
+            pool.run(b, [&](size_t i0, size_t i1) { for (size_t i = off + i0; i < off + i1; ++i) ptrs[i]->update_checksums(); });
+            return 0;
+        });
+    }
+    if (rc) {
+        std::printf("{\"error\": \"%s\"}\n", nfcs_strerror(rc));
+        return 1;
+    }
+    rp.clear();
+    rb.clear();
+    nfcs_device_free(c, d_arena);
+    nfcs_device_free(c, d_desc);
+    nfcs_host_free(c, h_ring);
+    std::printf("{\"ring_packets\": %zu, \"frame_bytes\": %.0f, \"threads\": %zu, \"seconds_per_leg\": %.2f, "
+                "\"reference_digest\": \"%s\", %s}\n",
+                n, frame_len, threads, seconds, want.c_str(), out.c_str());
+    return all_match ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (mode == "burstbench") {  // burstbench [sizes ring seconds threads want]
+        std::vector<size_t> sizes;
+        const std::string s = argc > 2 ? argv[2] : "64,256,1024,4096,16384,65536";
+        for (size_t p = 0; p < s.size();) {
+            const size_t q = s.find(',', p);
+            sizes.push_back(std::stoul(s.substr(p, q == std::string::npos ? std::string::npos : q - p)));
+            p = q == std::string::npos ? s.size() : q + 1;
+        }
+        return burstbench_mode(sizes, argc > 3 ? std::stoul(argv[3]) : (1u << 20), argc > 4 ? std::stod(argv[4]) : 0.4,
+                               argc > 5 ? std::stoul(argv[5]) : 16, argc > 6 ? argv[6] : "");
+    }
     if (mode == "adapterbench")
         return adapterbench_mode(argc > 2 ? std::stoul(argv[2]) : (1u << 20), argc > 3 ? std::stoul(argv[3]) : 3,
                                  argc > 4 ? std::stoul(argv[4]) : 16, argc > 5 ? argv[5] : "");

@@ -73,19 +73,21 @@ def test_host_path_argument_rules(engine):
 
 
 @pytest.mark.parametrize("n", [1, 70_000])
-def test_scattered_frame_larger_than_a_slot_is_rejected_untouched(engine, n):
-    """nfcs_update_host_frames checks every frame against the 64 MiB staging slot before anything is
-    staged (over the copy threads from 65,536 frames on): one frame claiming 64 MiB + 1 bytes makes
-    the call NFCS_EINVAL, and no frame is read or written (the frames here are 64-byte runts of one
-    small buffer; the oversized one points at it too)."""
+def test_scattered_frames_with_bad_arguments_are_rejected_untouched(engine, n):
+    """nfcs_update_host_frames rejects reserved flags and NULL arrays with NFCS_EINVAL before anything
+    is staged, and no frame is read or written (the frames here are 64-byte runts of one small
+    buffer). A frame longer than a 64 MiB staging slot is no longer an error: since round 6 it goes
+    as its first NFCS_FRAME_RELEVANT_BYTES, with the same result (test_gpu_host_ring.py
+    test_scattered_frames_longer_than_a_staging_slot)."""
     L = nf.lib()
     buf = np.random.default_rng(n).integers(0, 256, 64 * 16, dtype=np.uint8)
     before = buf.copy()
     ptrs = (buf.ctypes.data + (np.arange(n, dtype=np.uint64) % 16) * 64).astype(np.uint64)
     lens = np.full(n, 64, dtype=np.uint32)
-    lens[n // 2] = (64 << 20) + 1
     status = np.full(n, 0xAB, dtype=np.uint8)
-    assert L.nfcs_update_host_frames(engine.ctx, ptrs.ctypes.data, lens.ctypes.data, n, status.ctypes.data, 0) == EINVAL
+    assert L.nfcs_update_host_frames(engine.ctx, ptrs.ctypes.data, lens.ctypes.data, n, status.ctypes.data, 1) == EINVAL
+    assert L.nfcs_update_host_frames(engine.ctx, None, lens.ctypes.data, n, status.ctypes.data, 0) == EINVAL
+    assert L.nfcs_update_host_frames(engine.ctx, ptrs.ctypes.data, None, n, status.ctypes.data, 0) == EINVAL
     assert np.array_equal(buf, before)
     assert (status == 0xAB).all()
 

@@ -75,8 +75,9 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     h = d["host"]
     assert h["parity"]["match"] is True and h["pinned"]["GBps"] > 0 and h["pageable"]["GBps"] > 0
     # round 5: BASELINE C3's mix through the update and the fused forward, under the same clock
-    for k in ("c3", "l3fwd_c3"):
+    for k in ("c3", "l3fwd_c3", "c3_packed"):
         assert d[k]["parity"]["match"] is True and 0.2 < d[k]["frac"] < 1.0, (k, d[k])
+    assert d["c3_packed"]["frame_align"] == 16 and d["c3"]["frame_align"] == 128  # round 6: SURVEY's layout
     # and the reference's own call convention (one netflow::PacketBuffer per frame) end to end
     ha = d["host_adapter"]
     assert ha["rc"] == 0 and ha["parity"]["match"] is True and ha["adapter"]["GBps"] > 0, ha

@@ -238,3 +238,56 @@ def test_footprint_kept_per_burst_across_a_rotation(engine):
         for a, d, _ in bursts:
             a.free()
             d.free()
+
+
+def packed_udp(lengths, seed):
+    """IPv4/UDP frames of the given lengths, packed at 16-byte starts (SURVEY §8d's arena layout)."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for L in lengths:
+        f = rng.integers(0, 256, int(L), dtype=np.uint8)
+        f[12:16] = (0x08, 0x00, 0x45, 0x00)
+        f[16], f[17] = (L - 14) >> 8, (L - 14) & 0xFF
+        f[22], f[23] = 64, 17
+        f[38], f[39] = (L - 34) >> 8, (L - 34) & 0xFF
+        frames.append(f.tobytes())
+    return oracle.pack_frames(frames, align=16)
+
+
+@pytest.mark.parametrize("mix", ["c3", "imix"])
+def test_packed_mix_shape_follows_its_sample(engine, mix):
+    """A densely packed burst whose arena_bytes / n says 8-lane rows (< kTinyMeanBytes): the first call
+    runs them and samples its frames. C3's mix (U{64..1500}, 782 B per packet packed; half its frames
+    need a second 8-lane row pass) then runs the 16-lane short shape (footprint read back >= 800:
+    round 6, packed C3 0.655 against 0.79-0.82 ms per call in 8-lane rows); IMIX 7:4:1 (64/570/1500 B,
+    one frame in 12 longer than a row pass) stays on 8-lane rows. Bytes and statuses equal the
+    oracle's at every call (the shape picks speed only)."""
+    n = 1 << 17
+    if mix == "c3":
+        arena, desc = oracle.gen_config(3, 20250620, 0, n)
+    else:
+        lens = np.random.default_rng(62).permutation(np.tile([64] * 7 + [570] * 4 + [1500], n // 12 + 1)[:n])
+        arena, desc = packed_udp(lens, 61)
+    est = arena.nbytes // n
+    assert est < 800, est
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    engine.set_slot_bytes(0)
+    a = engine.alloc(arena.nbytes).upload(arena)
+    d = engine.alloc(desc.nbytes).upload(desc)
+    st = engine.alloc(n)
+    try:
+        assert engine.launch_footprint(arena.nbytes, d, n) == est  # nothing sampled: 8-lane rows
+        for k in range(3):
+            engine.update_device(a, arena.nbytes, d, n, st)
+            engine.sync()
+            assert np.array_equal(a.download(np.uint8, arena.nbytes), ref), k
+            assert np.array_equal(st.download(np.uint8, n), rst), k
+            fp = engine.launch_footprint(arena.nbytes, d, n)
+            if mix == "c3":
+                assert 800 <= fp < 1200, fp  # the short shape from the second call on
+            else:
+                assert fp < 800, fp  # 8-lane rows stay
+    finally:
+        for b in (a, d, st):
+            b.free()

@@ -31,4 +31,26 @@ call_a() {
     bash tools/pmc.sh r6a/pmc_c3p --config 3 --align 16 --steps 10 --no-host --no-c4 --no-replay
 }
 
+
+
+call_b() {
+  # round 6, GPU call b: packed C3 ran the tiny shape (8-lane rows: its 782-byte mean footprint is under
+  # kTinyMeanBytes, call a); the same batches in the short and long shapes by slot hint, alternating
+  local o=gpurun_out/r6b; mkdir -p $o
+  ab_lines $o 2 "cur" "c3p_auto --config 3 --align 16 --steps 40" "c3p_short --config 3 --align 16 --steps 40 --slot-bytes 900" \
+    "c3p_long --config 3 --align 16 --steps 40 --slot-bytes 1536" "c3a64 --config 3 --align 64 --steps 40" \
+    "c3a64_short --config 3 --align 64 --steps 40 --slot-bytes 900"
+}
+
+call_c() {
+  # round 6, GPU call c: the packed-mix shape rule (sample_footprint counts frames past one 8-lane row
+  # pass; kTinyLongMax): the GPU tests of the launch shapes and the host ring; packed C3 by default shape
+  # against the short-shape hint, alternating; the default bench line (its new c3_packed sub-line)
+  local o=gpurun_out/r6c; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py \
+    -q -x --timeout 120 --timeout-method thread > $o/pytest.log 2>&1 && \
+  ab_lines $o 2 "cur" "c3p_auto --config 3 --align 16 --steps 40" "c3p_short --config 3 --align 16 --steps 40 --slot-bytes 900" \
+    "l3c3p_auto --op l3fwd --config 3 --align 16 --steps 40" "l3c3_auto --op l3fwd --config 3 --align 128 --steps 40" && \
+  timeout -k 10 400 python3 -u bench.py --no-ops > $o/bench_default.json 2> $o/bench_default.err
+}
 "call_$1"
