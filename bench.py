@@ -145,6 +145,15 @@ class Dist:
         self.dist.all_gather(out, self._t(float(v)))
         return [float(x.item()) for x in out]
 
+    def gather_u64(self, v: int) -> list:
+        """Every rank's u64, exact (an int64 all-gather in two's complement)."""
+        s = int(v) % (1 << 64)
+        if self.ws == 1:
+            return [s]
+        out = [self._t(0, self.torch.int64) for _ in range(self.ws)]
+        self.dist.all_gather(out, self._t(s - (1 << 64) if s >= (1 << 63) else s, self.torch.int64))
+        return [int(x.item()) % (1 << 64) for x in out]
+
     def close(self):
         if self.ws > 1:
             self.dist.destroy_process_group()
@@ -471,10 +480,11 @@ def main():
     # process, run before this one touches the GPU, so its host copy threads have the host to themselves
     # (run after the device-resident lines, the same binary measured 29 against 47 GB/s standalone:
     # profiles/r05_b_*)
-    host_adapter = None
+    host_adapter = host_bursts = None
     if (ws == 1 and args.op == "update" and args.config == 1 and not args.packets and not args.no_c4
             and not args.no_host):
         host_adapter = host_adapter_line(DEFAULT_PACKETS[1])
+        host_bursts = host_bursts_line(DEFAULT_PACKETS[1])
     # NFCS_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a 1-GPU box
     dev = int(os.environ.get("NFCS_BENCH_DEVICE", local))
     if not torch_device_init(dev):
@@ -727,6 +737,16 @@ def main():
     }
     if ws > 1:
         out["per_gpu_GBps"] = [round(x, 1) for x in rank_gbps]  # each rank's own rate, this run
+        # each rank's own roofline: its calls timed by HIP events on its own
+        # engine's stream (the same rotation as rank 0's `roofline`, after the concurrent region), its
+        # kernel-time fraction of 8 TB/s, and the digest of what it updated — so a GPU that lags, or
+        # one whose result differs, shows by index, not only as lower efficiency
+        out["per_gpu_kernel_ms"] = [round(x, 4) for x in D.gather(ev_ms)]
+        out["per_gpu_frac"] = [round(x, 4) for x in D.gather(achieved / HBM_PEAK_GBS)]
+        hexd = got if len(got) == 16 and all(ch in "0123456789abcdef" for ch in got) else None
+        out["per_gpu_digest"] = [f"{x:016x}" for x in D.gather_u64(int(hexd, 16) if hexd else 0)]
+        out["per_gpu_parity"] = [None if x < 0 else bool(x) for x in
+                                 D.gather(-1.0 if parity_ok is None else float(bool(parity_ok)))]
     if solo is not None:
         # the same shard on one GPU in this run (rank 0, alone), and value / (N x that)
         out["single_gpu_same_shard_GBps"] = round(solo, 2)
@@ -779,6 +799,8 @@ def main():
             out["host"] = host_line(eng, args, n)
             if host_adapter is not None:
                 out["host_adapter"] = host_adapter
+            if host_bursts is not None:
+                out["host_bursts"] = host_bursts
         if not args.no_ops:
             out["more"] = more_lines(args)
     if rank == 0 and ws == 1 and not args.no_cpu:
@@ -1108,6 +1130,52 @@ def host_adapter_line(n: int):
     out["parity"] = {"reference_digest": want,
                      "match": all(out.get(k, {}).get("match") for k in
                                   ("adapter", "buffer_pool", "reference_1_thread", "reference_threads"))}
+    return out
+
+
+BURST_SIZES = (64, 256, 1024, 4096, 16384, 65536)
+
+
+def host_bursts_line(ring: int, sizes=BURST_SIZES, seconds: float = 0.4):
+    """The per-RX-burst operating point INTEGRATION.md §2 prescribes: a ring of C1
+    frames checksummed in consecutive bursts of b packets for each b in `sizes` — through
+    netflow_amd::update_checksums_batch on the reference's own netflow::PacketBuffers (`adapter`),
+    through nfcs_update_host on a pinned ring (`pinned_ring`, and its zero-copy form), and by the
+    reference's per-packet Packet::update_checksums() on 1 thread (the switch's own loop,
+    switch.hpp:213-294) and on as many threads as the cgroup grants (16 at most); µs per call (median of
+    every call in `seconds` per leg), GB/s, and the ring's digest per path against the reference's.
+    `crossover_vs_reference_1_thread`: the smallest burst at which the adapter path's median call is
+    shorter than the reference's own loop over the same burst. A child process (tests/cpp/_ref/
+    netflow_adapter_test burstbench), run before this process touches the GPU. Never `value`."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_ref", "netflow_adapter_test")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} missing (built by __graft_entry__.build() where /root/reference is)"}
+    quota = cgroup_cpu_quota()
+    threads = max(1, min(16, int(quota) if quota else len(allotted_cpus())))
+    want = golden_digest(1, 0, ring) or ""
+    try:
+        r = subprocess.run([exe, "burstbench", ",".join(str(b) for b in sizes), str(ring), str(seconds), str(threads),
+                            want], capture_output=True, text=True, timeout=400)
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        return {"error": repr(e)}
+    out["rc"] = r.returncode
+    paths = [k for k, v in out.items() if isinstance(v, dict) and "bursts" in v]
+    out["parity"] = {"reference_digest": want, "match": bool(paths) and all(out[k]["match"] for k in paths)}
+
+    def crossover(path, ref):
+        try:
+            return next((b for b in sizes if out[path]["bursts"][str(b)]["us_per_call"]
+                         < out[ref]["bursts"][str(b)]["us_per_call"]), None)
+        except KeyError:
+            return None
+    out["crossover_vs_reference_1_thread"] = {p: crossover(p, "reference_1_thread")
+                                              for p in ("adapter", "pinned_ring", "pinned_ring_zero_copy")}
+    out["crossover_vs_reference_threads"] = {p: crossover(p, "reference_threads")
+                                             for p in ("adapter", "pinned_ring", "pinned_ring_zero_copy")}
+    out["workload"] = (f"C1 frames (1500 B IPv4+UDP) in a ring of {human(ring)}, checksummed in consecutive bursts "
+                       f"of {', '.join(str(b) for b in sizes)} packets")
+    out["timing"] = "steady clock per call; median (and 10th percentile) of every call in the leg"
     return out
 
 

@@ -32,6 +32,10 @@
 // fewer than 16 bytes) are skipped: there the reference is undefined.
 #include <netflow++/packet.hpp>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -875,11 +879,12 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
     std::string out;
     bool all_match = true;
     auto path = [&](const char* name, bool ring_arena, const std::function<int(size_t, size_t)>& call) -> int {
+        std::fprintf(stderr, "burstbench: %s\n", name);
         restore(ring_arena);
         std::string legs;
-        size_t off = 0;
         for (size_t b : sizes) {
             if (b == 0 || n % b) return NFCS_EINVAL;
+            size_t off = 0;  // bursts of b packets at multiples of b: never past the ring's end
             std::vector<double> us;
             int r = call(off, b);  // warm: staging ring, pinned buffers, code, the workers
             off = (off + b) % n;
@@ -952,6 +957,11 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (mode == "burstbench") {  // burstbench [sizes ring seconds threads want]
+        signal(SIGSEGV, [](int) {  // a host-side fault: its stack to stderr (diagnostics only)
+            void* bt[64];
+            backtrace_symbols_fd(bt, backtrace(bt, 64), 2);
+            _exit(139);
+        });
         std::vector<size_t> sizes;
         const std::string s = argc > 2 ? argv[2] : "64,256,1024,4096,16384,65536";
         for (size_t p = 0; p < s.size();) {

@@ -35,9 +35,10 @@ def _worker(rank, ws, port, q):
     din, dout, hist = oracle.config_digest(1, bench.SEED, first, n, 1)
     dsum = D.sum(float(dout % (1 << 40)))  # exact in float64 for 2 ranks
     dsum64 = D.sum_u64(dout)
+    per = D.gather_u64(dout)  # the N > 1 line's per_gpu_digest (round 6)
     D.barrier()
     D.close()
-    q.put((rank, first, n, mx, total, dout, dsum, dsum64))
+    q.put((rank, first, n, mx, total, dout, dsum, dsum64, per))
 
 
 @pytest.mark.parametrize("ws", [2])
@@ -63,6 +64,7 @@ def test_two_rank_gloo_harness(ws):
     assert (sum(r[5] for r in res) % (1 << 64)) == whole
     assert all(r[6] == float(sum(x[5] % (1 << 40) for x in res)) for r in res)
     assert all(r[7] == whole for r in res)  # the exact u64 all-reduce
+    assert all(r[8] == [x[5] for x in res] for r in res)  # the exact u64 all-gather, in rank order
 
 
 def _strong_worker(rank, ws, port, q):

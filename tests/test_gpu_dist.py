@@ -42,6 +42,12 @@ def test_two_ranks_one_gpu_bench_line():
     assert d["parity"]["match"] is True and d["parity"]["all_ranks"] is True
     assert d["value"] > 0 and d["roofline"]["kernel_ms"] > 0
     assert len(d["per_gpu_GBps"]) == 2
+    # round 6: every rank's own roofline and digest, by index
+    assert len(d["per_gpu_frac"]) == 2 and all(0 < f < 1.0 for f in d["per_gpu_frac"])
+    assert len(d["per_gpu_kernel_ms"]) == 2 and all(t > 0 for t in d["per_gpu_kernel_ms"])
+    assert d["per_gpu_frac"][0] == d["roofline"]["frac"]
+    assert d["per_gpu_parity"] == [True, True]
+    assert d["per_gpu_digest"][0] == d["parity"]["digest"] and len(set(d["per_gpu_digest"])) == 2
     # the same shard on one GPU, timed alone in the same run, and the efficiency against it (both
     # ranks share cuda:0 here, so about 0.5)
     assert d["single_gpu_same_shard_GBps"] > 0

@@ -53,4 +53,34 @@ call_c() {
     "l3c3p_auto --op l3fwd --config 3 --align 16 --steps 40" "l3c3_auto --op l3fwd --config 3 --align 128 --steps 40" && \
   timeout -k 10 400 python3 -u bench.py --no-ops > $o/bench_default.json 2> $o/bench_default.err
 }
+
+call_d() {
+  # round 6, GPU call d: the per-RX-burst operating point: burstbench alone, then the
+  # host lines of the default bench (host, host_adapter, host_bursts)
+  local o=gpurun_out/r6d; mkdir -p $o
+  timeout -k 10 300 tests/cpp/_ref/netflow_adapter_test burstbench 64,256,1024,4096,16384,65536 1048576 0.4 16 81cc3905092d7f44 \
+    > $o/burstbench.json 2> $o/burstbench.err
+}
+
+call_e() {
+  # round 6, GPU call e: burstbench's host-side fault of call d, with a stack dump and progress lines
+  local o=gpurun_out/r6e; mkdir -p $o
+  timeout -k 10 120 tests/cpp/_ref/netflow_adapter_test burstbench 256,4096 65536 0.1 16 ffffffffffffffff > $o/burstbench_small.json 2> $o/burstbench_small.err
+  echo "rc=$?" >> $o/burstbench_small.err
+}
+
+call_f() {
+  # round 6, GPU call f: direct chunks (no DMA for chunks of <= 2 MiB) and the lower host-copy split
+  # thresholds: the host-path GPU tests, then burstbench per library (pre = before the change; d0 = the
+  # change without direct chunks; d8 = direct chunks up to 8 MiB), alternating, two rounds
+  local o=gpurun_out/r6f; mkdir -p $o
+  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_netflow_adapter.py \
+    tests/test_gpu_parity.py tests/test_gpu_large_arena.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 || return 1
+  local r lib exe
+  for r in 1 2; do for lib in cur pre d0 d8; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 64,256,1024,4096,16384,65536 1048576 0.4 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+}
 "call_$1"

@@ -139,8 +139,6 @@ struct nfcs_ctx {
     nfcs_desc* d_desc[kSlots] = {nullptr, nullptr};
     uint8_t* d_status[kSlots] = {nullptr, nullptr};
     nfcs_patch* d_patch[kSlots] = {nullptr, nullptr};
-    uint8_t* z_block[kSlots] = {nullptr, nullptr};  // the pinned block of each slot as the GPU addresses it
-                                                    // (direct chunks; null: not mapped, DMA only)
     uint8_t* h_arena[kSlots] = {nullptr, nullptr};  // pinned
     nfcs_desc* h_desc[kSlots] = {nullptr, nullptr};
     uint8_t* h_status[kSlots] = {nullptr, nullptr};
@@ -323,32 +321,6 @@ void host_block_free(HostBlock& b) {
     b = HostBlock{};
 }
 
-// A pointer into slot s's pinned block, as the GPU addresses it.
-template <class T>
-T* zdev(const nfcs_ctx* c, int s, T* host) {
-    return host ? reinterpret_cast<T*>(c->z_block[s] + (reinterpret_cast<const uint8_t*>(host) -
-                                                        static_cast<const uint8_t*>(c->hb[s].p)))
-                : nullptr;
-}
-
-// Direct chunks (round 6, VERDICT r5 item 2: the per-RX-burst operating point). A chunk of at most
-// kDirectChunkBytes of frames moves no DMA at all: the kernel reads its descriptors and frames where
-// the host left them (the slot's pinned block, or a pinned caller arena in place) and writes its patch
-// records and statuses straight into the slot's pinned block; the host waits for one event. At these
-// sizes a call is bound by fixed costs, and the three copy-engine transfers it saves (descriptors,
-// frames in, records out: each a queued DMA with its own setup latency) were most of them: 256 C1
-// frames through nfcs_update_host 49.5 µs per call with copies, 26.4 in the zero-copy form
-// (profiles/r06_host_bursts_*.json). Larger chunks keep the copy engines, which move bytes over PCIe
-// faster than kernel loads do (1M C1 frames: 51.7 against 43 GB/s zero-copy).
-#ifndef NFCS_DIRECT_CHUNK_BYTES
-#define NFCS_DIRECT_CHUNK_BYTES (2u << 20)
-#endif
-constexpr uint64_t kDirectChunkBytes = NFCS_DIRECT_CHUNK_BYTES;
-// Host copy work per thread before a copy is split over the workers (a worker's wake-up costs ~10 µs;
-// one thread stages ~15 GB/s): gathers and staging copies from 512 KiB, write-backs from 2048 frames.
-constexpr uint64_t kCopyBytesPerThread = 512u << 10;
-constexpr uint32_t kPatchFramesPerThread = 2048;
-
 // Host copies whose destination this CPU does not read again (the staging slots, which the copy
 // engine reads next; frames copied back into a caller's arena): 16-byte non-temporal stores, so a
 // destination line is written once instead of first being read for ownership (a plain memcpy of a
@@ -390,7 +362,7 @@ static inline void nt_fence() { __builtin_ia32_sfence(); }  // the non-temporal 
 // below what PCIe moves (e2e: pageable staging 27 GB/s single-threaded vs 54 GB/s pinned). The
 // workers run on the GPU's NUMA node, next to the staging memory.
 void par_memcpy(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
-    const size_t kMin = kCopyBytesPerThread;
+    const size_t kMin = 4u << 20;
     if (bytes < 2 * kMin || c->workers.size() == 0) {
         stream_copy((uint8_t*)dst, (const uint8_t*)src, bytes, false);
         nt_fence();
@@ -426,7 +398,6 @@ void free_host_pipeline(nfcs_ctx* c) {
         c->d_status[s] = nullptr;
         c->d_patch[s] = nullptr;
         c->h_arena[s] = nullptr;
-        c->z_block[s] = nullptr;
         c->h_desc[s] = nullptr;
         c->h_status[s] = nullptr;
         c->h_patch[s] = nullptr;
@@ -483,11 +454,6 @@ int build_host_pipeline(nfcs_ctx* ctx) {
         ctx->h_desc[s] = reinterpret_cast<nfcs_desc*>(p + ctx->stage_bytes);
         ctx->h_patch[s] = reinterpret_cast<nfcs_patch*>(p + ctx->stage_bytes + a_desc);
         ctx->h_status[s] = p + ctx->stage_bytes + a_desc + a_patch;
-        // the block as the GPU addresses it (registered and hipHostMalloc'd memory is mapped): direct
-        // chunks read their frames and descriptors and write their records and statuses here
-        void* zp = nullptr;
-        if (hipHostGetDevicePointer(&zp, p, 0) == hipSuccess) ctx->z_block[s] = static_cast<uint8_t*>(zp);
-        else (void)hipGetLastError();
     }
     ctx->numa_local = local;
     ctx->workers.start(ctx->copy_threads - 1, ctx->have_cpus ? &ctx->node_cpus : nullptr);
@@ -877,7 +843,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             // CPU has not cached: prefetch the line kPf packets ahead so the misses overlap; large
             // chunks over the workers
             const nfcs_patch* pq = c->h_patch[s];
-            const int np = std::min<int>(c->workers.size() + 1, std::max<uint32_t>(1, m / kPatchFramesPerThread));
+            const int np = m >= 16384 ? c->workers.size() + 1 : 1;
             c->workers.run(np, [&](int t) {
                 const uint32_t j0 = (uint32_t)((uint64_t)m * t / np), j1 = (uint32_t)((uint64_t)m * (t + 1) / np);
                 constexpr uint32_t kPf = 16;
@@ -944,17 +910,6 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint32_t m = i1 - i;
         const uint64_t bytes = end - base;
         const uint8_t* src = h_arena + base;
-        // a direct chunk (records back, small): no DMA; the kernel reads a pinned arena in place
-        uint8_t* zsrc = nullptr;
-        if (patch_only && c->z_block[s] && bytes <= kDirectChunkBytes) {
-            if (pinned) {
-                void* dp = nullptr;
-                if (hipHostGetDevicePointer(&dp, h_arena, 0) == hipSuccess) zsrc = static_cast<uint8_t*>(dp) + base;
-                else (void)hipGetLastError();
-            } else {
-                zsrc = zdev(c, s, c->h_arena[s]);
-            }
-        }
         if (!pinned) {
             par_memcpy(c, c->h_arena[s], src, bytes);
             src = c->h_arena[s];
@@ -965,21 +920,6 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             if (e != hipSuccess) break;
         }
         hipStream_t st = c->hs[s];
-        if (zsrc) {
-            e = nfcs::launch_update(c->di, zsrc, bytes ? bytes : 16, zdev(c, s, c->h_desc[s]), m, (uint32_t)(base >> 4),
-                                    h_status ? zdev(c, s, c->h_status[s]) : nullptr, zdev(c, s, c->h_patch[s]),
-                                    nullptr, nfcs::kUpdateRecords, st);
-            if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);  // the kernel read the slot
-            if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
-            if (e != hipSuccess) {
-                (void)hipStreamSynchronize(st);
-                break;
-            }
-            slot[s] = {i, i1, base, bytes, true};
-            i = i1;
-            s ^= 1;
-            continue;
-        }
         e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                            hipMemcpyHostToDevice, st);
         if (e == hipSuccess && bytes)
@@ -1080,7 +1020,7 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         if (e != hipSuccess) return;
         const uint32_t m = k.i1 - k.i0;
         const nfcs_patch* pt = c->h_patch[s];
-        const int np = std::min<int>(parts, std::max<uint32_t>(1, m / kPatchFramesPerThread));
+        const int np = m >= 16384 ? parts : 1;
         c->workers.run(np, [&](int t) {
             const uint32_t j0 = (uint32_t)((uint64_t)m * t / np), j1 = (uint32_t)((uint64_t)m * (t + 1) / np);
             constexpr uint32_t kPf = 16;  // the header lines of frames kPf ahead: their misses overlap
@@ -1116,7 +1056,7 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         }
         const uint32_t m = i1 - i;
         uint8_t* dst = c->h_arena[s];
-        const int ng = (int)std::min<uint64_t>(parts, std::max<uint64_t>(1, bytes / kCopyBytesPerThread));
+        const int ng = bytes >= (8u << 20) ? parts : 1;
         c->workers.run(ng, [&](int t) {
             const uint32_t j0 = (uint32_t)((uint64_t)m * t / ng), j1 = (uint32_t)((uint64_t)m * (t + 1) / ng);
             constexpr uint32_t kPf = 4;  // the first lines of the frame kPf ahead: its misses overlap this copy
@@ -1135,24 +1075,15 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         finish(s);  // chunk k-2: its records and statuses are read out of the slot before chunk k's land
         if (e != hipSuccess) break;
         hipStream_t st = c->hs[s];
-        if (c->z_block[s] && bytes <= kDirectChunkBytes) {
-            // a direct chunk: the kernel reads the gathered frames and descriptors in the pinned slot
-            // and writes records and statuses there; no DMA (kDirectChunkBytes)
-            e = nfcs::launch_update(c->di, zdev(c, s, dst), bytes ? bytes : 16, zdev(c, s, hd), m, 0u,
-                                    h_status ? zdev(c, s, c->h_status[s]) : nullptr, zdev(c, s, c->h_patch[s]),
-                                    nullptr, nfcs::kUpdateRecords, st);
-            if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
-        } else {
-            e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);
-            if (e == hipSuccess && bytes) e = hipMemcpyAsync(c->d_arena[s], dst, bytes, hipMemcpyHostToDevice, st);
-            if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
-            if (e == hipSuccess)
-                e = nfcs::launch_update(c->di, c->d_arena[s], bytes ? bytes : 16, c->d_desc[s], m, 0u, c->d_status[s],
-                                        c->d_patch[s], nullptr, nfcs::kUpdateRecords, st);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch), hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess && h_status) e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
-        }
+        e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(c->d_arena[s], dst, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
+        if (e == hipSuccess)
+            e = nfcs::launch_update(c->di, c->d_arena[s], bytes ? bytes : 16, c->d_desc[s], m, 0u, c->d_status[s],
+                                    c->d_patch[s], nullptr, nfcs::kUpdateRecords, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->h_patch[s], c->d_patch[s], (size_t)m * sizeof(nfcs_patch), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && h_status) e = hipMemcpyAsync(c->h_status[s], c->d_status[s], m, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
         if (e != hipSuccess) {
             (void)hipStreamSynchronize(st);  // whatever was queued on this slot has finished
