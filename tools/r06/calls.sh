@@ -83,4 +83,19 @@ call_f() {
       > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
   done; done
 }
+
+call_g() {
+  # round 6, GPU call g: the fused forward's bound on C3 (tools/r06/fwd_bound.py), its
+  # issue / stall counters beside the update's C3; the per-rank roofline of the N > 1 line (2-rank test, a
+  # 4-rank rehearsal on this one GPU); the default bench line with its host_bursts sub-line
+  local o=gpurun_out/r6g; mkdir -p $o
+  timeout -k 10 300 python3 -u tools/r06/fwd_bound.py --variants 0,1,2,3,4,5 --rounds 3 > $o/fwd_bound.jsonl 2> $o/fwd_bound.err && \
+  PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD;SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" \
+    bash tools/pmc.sh r6g/pmc_fwd_c3 --op l3fwd --config 3 --steps 10 --no-host --no-c4 --no-replay && \
+  PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD;SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" \
+    bash tools/pmc.sh r6g/pmc_upd_c3 --config 3 --steps 10 --no-host --no-c4 --no-replay && \
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dist.py -q -x --timeout 280 --timeout-method thread -k two_ranks_one_gpu > $o/pytest_dist.log 2>&1 && \
+  NFCS_BENCH_DEVICE=0 timeout -k 10 300 python3 -u bench.py --gpus 4 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus4_one_box.json 2> $o/bench_gpus4.err && \
+  timeout -k 10 500 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
 "call_$1"
