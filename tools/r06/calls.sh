@@ -98,4 +98,18 @@ call_g() {
   NFCS_BENCH_DEVICE=0 timeout -k 10 300 python3 -u bench.py --gpus 4 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus4_one_box.json 2> $o/bench_gpus4.err && \
   timeout -k 10 500 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
 }
+
+call_h() {
+  # round 6, GPU call h: every GPU test on the round-6 product; rocprofv3 stats of the default bench line
+  # and of packed C3; PMC traffic of packed C3 in its new shape (merged into a copy of profiles/traffic.json)
+  local o=gpurun_out/r6h; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 || return 1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$o/default" -o default -- \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu --no-ops > $o/default.json 2> $o/default.err || return 1
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$o/c3p" -o c3p -- \
+    python3 bench.py --config 3 --align 16 --steps 30 --no-cpu --no-replay --no-host --no-c4 > $o/c3p.json 2> $o/c3p.err || return 1
+  cp profiles/traffic.json $o/traffic_in.json
+  timeout -k 10 600 python3 tools/pmc_traffic.py --out "$PWD/$o/pmc" --configs 3 --align 16 --merge "$PWD/$o/traffic_in.json" \
+    > $o/pmc.log 2>&1
+}
 "call_$1"
