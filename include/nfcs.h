@@ -185,7 +185,8 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
  *                        are rewritten with the values read: not for a ring whose other slots
  *                        are being filled meanwhile — the default writes only checksum bytes)
  *   NFCS_HOST_ZERO_COPY  pinned arenas only: the kernel reads the frames over PCIe in place and
- *                        writes the checksum bytes straight back (no staging copies)
+ *                        writes the checksum bytes straight back (no staging copies); the default
+ *                        form for pinned bursts of up to 32 MiB (round 6: one launch, no DMA)
  *   NFCS_HOST_PATCH_ONLY the default since ABI 1 session 2; accepted and ignored
  * Rates: DESIGN.md §7. */
 #define NFCS_HOST_PATCH_ONLY 1u

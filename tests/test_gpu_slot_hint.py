@@ -291,3 +291,48 @@ def test_packed_mix_shape_follows_its_sample(engine, mix):
     finally:
         for b in (a, d, st):
             b.free()
+
+
+def test_packed_mix_forward_and_vlan_follow_the_sample(engine):
+    """The same shape rule for the fused L3 forward and VLAN push/pop (their launches sample too): C3's
+    mix packed at 16-byte starts, three forwards in a row (8-lane rows of 6 slots, then the short-mix
+    shape once the sample has counted the long frames) and a push / pop / push sequence, each call's
+    bytes, statuses and lengths against the oracle applied as many times."""
+    n = 1 << 16
+    arena0, desc0 = oracle.gen_config(3, 20250620, 0, n)
+    frames = oracle.unpack_frames(arena0, desc0)
+    arena, desc = oracle.pack_frames(frames, align=16, room=4)
+    caps = np.diff(np.append(desc["off16"].astype(np.int64), arena.nbytes // 16)) * 16
+    rng = np.random.default_rng(63)
+    table = rng.integers(0, 256, (8, 12), dtype=np.uint8)
+    nh = (np.arange(n) % 9).astype(np.uint32)  # index 8: no route
+    engine.set_slot_bytes(0)
+    d_arena = engine.alloc(arena.nbytes).upload(arena)
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_nh = engine.alloc(4 * n).upload(nh)
+    d_tab = engine.alloc(table.nbytes).upload(table)
+    d_caps = engine.alloc(8 * n).upload(np.ascontiguousarray(caps, dtype=np.uint32))
+    d_st = engine.alloc(n)
+    try:
+        assert engine.launch_footprint(arena.nbytes, d_desc, n) < 800
+        ref = arena.copy()
+        for k in range(3):
+            rst = oracle.l3_forward_batch(ref, desc, nh, table)
+            engine.l3_forward_device(d_arena, arena.nbytes, d_desc, d_nh, n, d_tab, 8, d_st)
+            engine.sync()
+            assert np.array_equal(d_st.download(np.uint8, n), rst), k
+            assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), k
+        assert engine.launch_footprint(arena.nbytes, d_desc, n) >= 800  # the forward's sample moved it
+        rdesc = desc.copy()
+        for k, op in enumerate(["push", "pop", "push"]):
+            word = oracle.vlan_op(op, 100 + k, 3)
+            rst = oracle.vlan_batch(ref, rdesc, None, caps, op_all=word)
+            engine.vlan_device(d_arena, arena.nbytes, d_desc, n, None, word, d_caps, 0, d_st)
+            engine.sync()
+            assert np.array_equal(d_st.download(np.uint8, n), rst), op
+            assert np.array_equal(d_desc.download(np.dtype(desc.dtype), n), rdesc), op
+            assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), op
+    finally:
+        engine.set_slot_bytes(0)
+        for b in (d_arena, d_desc, d_nh, d_tab, d_caps, d_st):
+            b.free()

@@ -5,6 +5,9 @@
 # netflow_adapter_test burstbench binary linked to it (tests/cpp/_ref/netflow_adapter_test_<name>).
 set -euo pipefail
 cd "$(dirname "$0")/../.."
+# the sources before direct chunks, from git (not kept in the tree)
+mkdir -p tools/r06/pre_src
+for f in nfcs_api.hip nfcs_kernels.hip nfcs_internal.h; do git show a4256f8:netflow_amd/csrc/$f > tools/r06/pre_src/$f; done
 HIPCC="hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -mllvm -amdgpu-kernarg-preload-count=8 -Iinclude"
 one() {  # one NAME SRC [defines]
   local name=$1 src=$2; shift 2

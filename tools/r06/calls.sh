@@ -112,4 +112,26 @@ call_h() {
   timeout -k 10 600 python3 tools/pmc_traffic.py --out "$PWD/$o/pmc" --configs 3 --align 16 --merge "$PWD/$o/traffic_in.json" \
     > $o/pmc.log 2>&1
 }
+
+call_i() {
+  # round 6, GPU call i: where a per-RX-burst call's time goes (tools/r06/host_lat.hip)
+  local o=gpurun_out/r6i; mkdir -p $o
+  timeout -k 10 120 tools/r06/host_lat > $o/host_lat.json 2> $o/host_lat.err
+}
+
+call_j() {
+  # round 6, GPU call j: pinned bursts of <= 32 MiB run zero-copy by default, zero-copy descriptors and
+  # statuses through the slot's pinned block: the host-path GPU tests, host_lat, then burstbench against the
+  # library before the change (direct = git 4f91a02), alternating, two rounds
+  local o=gpurun_out/r6j; mkdir -p $o
+  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_netflow_adapter.py \
+    tests/test_gpu_parity.py tests/test_gpu_large_arena.py tests/test_gpu_slot_hint.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 || return 1
+  timeout -k 10 120 tools/r06/host_lat > $o/host_lat.json 2> $o/host_lat.err || return 1
+  local r lib exe
+  for r in 1 2; do for lib in cur direct; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 64,256,1024,4096,16384,65536 1048576 0.4 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+}
 "call_$1"
