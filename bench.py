@@ -1136,7 +1136,7 @@ def host_adapter_line(n: int):
 BURST_SIZES = (64, 256, 1024, 4096, 16384, 65536)
 
 
-def host_bursts_line(ring: int, sizes=BURST_SIZES, seconds: float = 0.4):
+def host_bursts_line(ring: int, sizes=BURST_SIZES, seconds: float = 0.25):
     """The per-RX-burst operating point INTEGRATION.md §2 prescribes: a ring of C1
     frames checksummed in consecutive bursts of b packets for each b in `sizes` — through
     netflow_amd::update_checksums_batch on the reference's own netflow::PacketBuffers (`adapter`),

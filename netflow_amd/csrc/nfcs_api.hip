@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -139,6 +140,14 @@ struct nfcs_ctx {
     nfcs_desc* d_desc[kSlots] = {nullptr, nullptr};
     uint8_t* d_status[kSlots] = {nullptr, nullptr};
     nfcs_patch* d_patch[kSlots] = {nullptr, nullptr};
+    // direct chunks' completion flags (nfcs::DoneReq): per slot a host-mapped word on its own 64-byte
+    // line (done_host[8 s]), a device counter of finished workgroups, and the count the slot's next
+    // launch starts from; wait_for[s] != 0: the chunk in slot s signals through its flag
+    uint64_t* done_host = nullptr;
+    uint64_t* done_dev = nullptr;
+    uint64_t* done_ctr = nullptr;
+    uint64_t done_base[kSlots] = {0, 0};
+    int slot_wait[kSlots] = {0, 0};  // 0: the slot's chunk is waited for on its event; 1: on its flag; 2: flag seen
     uint8_t* z_block[kSlots] = {nullptr, nullptr};  // the pinned block of each slot as the GPU addresses it
                                                     // (direct chunks; null: not mapped, DMA only)
     uint8_t* h_arena[kSlots] = {nullptr, nullptr};  // pinned
@@ -413,6 +422,15 @@ void par_memcpy(nfcs_ctx* c, void* dst, const void* src, size_t bytes) {
 void free_host_pipeline(nfcs_ctx* c) {
     c->host_ready = false;
     c->workers.stop();
+    if (c->done_host) {
+        for (int s = 0; s < nfcs_ctx::kSlots; ++s)
+            if (c->hs[s]) (void)hipStreamSynchronize(c->hs[s]);  // no launch still counting into them
+        (void)hipHostFree(c->done_host);
+    }
+    if (c->done_ctr) (void)hipFree(c->done_ctr);
+    c->done_host = nullptr;
+    c->done_dev = nullptr;
+    c->done_ctr = nullptr;
     for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
         if (c->hs[s]) { (void)hipStreamSynchronize(c->hs[s]); (void)hipStreamDestroy(c->hs[s]); }
         if (c->done[s]) (void)hipEventDestroy(c->done[s]);
@@ -438,6 +456,44 @@ void free_host_pipeline(nfcs_ctx* c) {
 }
 
 int build_host_pipeline(nfcs_ctx* ctx);
+
+// A direct chunk's completion request for slot s (nfcs::DoneReq), or none where the context has no flags.
+nfcs::DoneReq done_req(nfcs_ctx* c, int s) {
+    c->slot_wait[s] = c->done_host ? 1 : 0;
+    if (!c->done_host) return {};
+    return {c->done_dev + 8 * s, c->done_ctr + s, c->done_base[s]};
+}
+// The chunk launched in slot s is waited for on its events.
+void event_wait(nfcs_ctx* c, int s) { c->slot_wait[s] = 0; }
+
+// Waits for the chunk in slot s: on its completion flag when it has one (a direct chunk: the kernel's
+// last workgroup publishes the count; once seen, later waits for the same chunk return at once), else
+// — or after kFlagSpinNs without the flag, e.g. a launch that failed — on the event.
+hipError_t wait_slot(nfcs_ctx* c, int s, hipEvent_t ev) {
+    constexpr int64_t kFlagSpinNs = 20000000;
+    if (c->slot_wait[s] == 2) return hipSuccess;
+    if (c->slot_wait[s] == 1) {
+        const uint64_t base = c->done_base[s];
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 1;; ++k) {
+            const uint64_t v = __atomic_load_n(c->done_host + 8 * s, __ATOMIC_ACQUIRE);
+            if (v > base) {
+                c->done_base[s] = v;
+                c->slot_wait[s] = 2;
+                return hipSuccess;
+            }
+            if ((k & 1023u) == 0 &&
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kFlagSpinNs)
+                break;
+            __builtin_ia32_pause();
+        }
+        const hipError_t e = hipEventSynchronize(ev);
+        c->done_base[s] = std::max(c->done_base[s], __atomic_load_n(c->done_host + 8 * s, __ATOMIC_ACQUIRE));
+        c->slot_wait[s] = 0;
+        return e;
+    }
+    return hipEventSynchronize(ev);
+}
 
 // The host pipeline, built on first use on the context's device (the caller holds a DeviceGuard).
 // A build that fails part-way is torn down, so the next call retries it instead of using half of it.
@@ -494,6 +550,24 @@ int build_host_pipeline(nfcs_ctx* ctx) {
         else (void)hipGetLastError();
     }
     ctx->numa_local = local;
+    // completion flags of direct chunks: optional (without them the chunks wait on their events)
+    if (hipHostMalloc((void**)&ctx->done_host, nfcs_ctx::kSlots * 64, hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer((void**)&ctx->done_dev, ctx->done_host, 0) == hipSuccess &&
+        hipMalloc((void**)&ctx->done_ctr, nfcs_ctx::kSlots * sizeof(uint64_t)) == hipSuccess &&
+        hipMemset(ctx->done_ctr, 0, nfcs_ctx::kSlots * sizeof(uint64_t)) == hipSuccess) {
+        memset(ctx->done_host, 0, nfcs_ctx::kSlots * 64);
+    } else {
+        (void)hipGetLastError();
+        if (ctx->done_host) (void)hipHostFree(ctx->done_host);
+        if (ctx->done_ctr) (void)hipFree(ctx->done_ctr);
+        ctx->done_host = nullptr;
+        ctx->done_dev = nullptr;
+        ctx->done_ctr = nullptr;
+    }
+    for (int s = 0; s < nfcs_ctx::kSlots; ++s) {
+        ctx->done_base[s] = 0;
+        ctx->slot_wait[s] = 0;
+    }
     ctx->workers.start(ctx->copy_threads - 1, ctx->have_cpus ? &ctx->node_cpus : nullptr);
     return NFCS_OK;
 }
@@ -541,7 +615,7 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
     // wait for slot s; its statuses are copied out only while no error has occurred
     auto finish = [&](int s) {
         if (!cnt[s]) return;
-        const hipError_t f = hipEventSynchronize(c->done[s]);
+        const hipError_t f = wait_slot(c, s, c->done[s]);
         if (e == hipSuccess) e = f;
         if (e == hipSuccess && h_status) memcpy(h_status + first[s], c->h_status[s], cnt[s]);
         cnt[s] = 0;
@@ -555,15 +629,20 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
         memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
         // the launch shape follows this chunk's own frames (their span per packet, over the runs of
         // a burst that wraps its ring), not the caller's whole arena, unless the context has a hint
+        const uint64_t span = run_span(h_desc, i, i + m, arena_bytes);
         uint64_t shape = c->slot_bytes;
-        if (!shape) shape = std::max<uint64_t>(1, run_span(h_desc, i, i + m, arena_bytes) / m);
+        if (!shape) shape = std::max<uint64_t>(1, span / m);
         if (c->z_block[s]) {
             // round 6: the kernel reads the chunk's descriptors from the slot's pinned block and writes
-            // its statuses there (no DMA at all: burst sizes where the call is bound by fixed costs)
+            // its statuses there (no DMA at all: burst sizes where the call is bound by fixed costs); a
+            // small chunk signals its completion through the slot's flag (nfcs::DoneReq)
+            const nfcs::DoneReq dr = span <= kDirectChunkBytes ? done_req(c, s) : nfcs::DoneReq{};
+            if (!dr.flag) event_wait(c, s);
             e = nfcs::launch_update(c->di, d_arena, arena_bytes, zdev(c, s, c->h_desc[s]), m, 0u,
                                     h_status ? zdev(c, s, c->h_status[s]) : nullptr, nullptr, nullptr,
-                                    nfcs::kUpdateInline, st, shape);
+                                    nfcs::kUpdateInline, st, shape, {}, dr);
         } else {
+            event_wait(c, s);
             e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                                hipMemcpyHostToDevice, st);
             if (e == hipSuccess)
@@ -888,7 +967,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         Chunk& k = slot[s];
         if (!k.used) return;
         k.used = false;
-        const hipError_t f = hipEventSynchronize(c->done[s]);
+        const hipError_t f = wait_slot(c, s, c->done[s]);
         if (e == hipSuccess) e = f;
         if (e != hipSuccess) return;
         const uint32_t m = k.i1 - k.i0;
@@ -958,7 +1037,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         if (!patch_only) {
             finish(s);
         } else if (slot[s].used) {
-            e = hipEventSynchronize(c->staged[s]);
+            e = wait_slot(c, s, c->staged[s]);
         }
         if (e != hipSuccess) break;
         const uint32_t m = i1 - i;
@@ -988,7 +1067,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         if (zsrc) {
             e = nfcs::launch_update(c->di, zsrc, bytes ? bytes : 16, zdev(c, s, c->h_desc[s]), m, (uint32_t)(base >> 4),
                                     h_status ? zdev(c, s, c->h_status[s]) : nullptr, zdev(c, s, c->h_patch[s]),
-                                    nullptr, nfcs::kUpdateRecords, st);
+                                    nullptr, nfcs::kUpdateRecords, st, 0, {}, done_req(c, s));
             if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);  // the kernel read the slot
             if (e == hipSuccess) e = hipEventRecord(c->done[s], st);
             if (e != hipSuccess) {
@@ -1000,6 +1079,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             s ^= 1;
             continue;
         }
+        event_wait(c, s);
         e = hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(nfcs_desc),
                            hipMemcpyHostToDevice, st);
         if (e == hipSuccess && bytes)
@@ -1095,7 +1175,7 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         Chunk& k = slot[s];
         if (!k.used) return;
         k.used = false;
-        const hipError_t f = hipEventSynchronize(c->done[s]);
+        const hipError_t f = wait_slot(c, s, c->done[s]);
         if (e == hipSuccess) e = f;
         if (e != hipSuccess) return;
         const uint32_t m = k.i1 - k.i0;
@@ -1119,7 +1199,7 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
     int s = 0;
     while (i < n && e == hipSuccess) {
         if (slot[s].used) {  // chunk k-2's copies in are done: its arena and descriptors are free
-            e = hipEventSynchronize(c->staged[s]);
+            e = wait_slot(c, s, c->staged[s]);
             if (e != hipSuccess) break;
         }
         // next chunk: packets [i, i1), their 16-byte padded frames within chunk_target bytes (at
@@ -1160,9 +1240,10 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
             // and writes records and statuses there; no DMA (kDirectChunkBytes)
             e = nfcs::launch_update(c->di, zdev(c, s, dst), bytes ? bytes : 16, zdev(c, s, hd), m, 0u,
                                     h_status ? zdev(c, s, c->h_status[s]) : nullptr, zdev(c, s, c->h_patch[s]),
-                                    nullptr, nfcs::kUpdateRecords, st);
+                                    nullptr, nfcs::kUpdateRecords, st, 0, {}, done_req(c, s));
             if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);
         } else {
+            event_wait(c, s);
             e = hipMemcpyAsync(c->d_desc[s], hd, (size_t)m * sizeof(nfcs_desc), hipMemcpyHostToDevice, st);
             if (e == hipSuccess && bytes) e = hipMemcpyAsync(c->d_arena[s], dst, bytes, hipMemcpyHostToDevice, st);
             if (e == hipSuccess) e = hipEventRecord(c->staged[s], st);

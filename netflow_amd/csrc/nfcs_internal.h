@@ -110,10 +110,23 @@ struct ObsReq {
     uint64_t tag = 0;
 };
 
+// A completion request (round 6, the host path's small chunks): every workgroup counts itself in *ctr
+// (device memory) once its stores have been released at system scope; the one that brings the count to
+// base + gridDim.x (base: the count before this launch, which the host tracks) stores that count into
+// *flag (host-mapped) with a system-scope release, and the host spins on *flag instead of waiting for the
+// stream's event. The count only grows, so a flag above base means this launch is done, and no reset
+// (no extra launch) is needed between launches. Only for launches of kUpdateRecords / kUpdateInline (one
+// kernel per call). flag null: none.
+struct DoneReq {
+    uint64_t* flag = nullptr;
+    uint64_t* ctr = nullptr;
+    uint64_t base = 0;
+};
+
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
-                         uint64_t slot_bytes = 0, ObsReq obs = {});
+                         uint64_t slot_bytes = 0, ObsReq obs = {}, DoneReq done = {});
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                              const nfcs_desc* desc, const uint32_t* nh, uint32_t n,

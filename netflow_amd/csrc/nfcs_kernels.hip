@@ -692,7 +692,25 @@ struct FwdArgs {
     const nfcs_nexthop* table;
     uint32_t table_n;
     ObsReq obs;
+    DoneReq done = {};
 };
+
+// DoneReq (nfcs_internal.h): every wave of the workgroup has issued its stores (the barrier); one lane
+// releases them at system scope and counts the workgroup (a vector atomic); the workgroup that completes
+// the count publishes it with a system-scope release store (a vector store), which the host's acquire
+// load of the flag pairs with. Waves that had no packets reach the barrier too (update_rows_kernel
+// returns early only without a DoneReq).
+DEV void signal_done(const DoneReq& d, uint32_t nblocks) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this workgroup's frame / record stores
+        const uint64_t now = __hip_atomic_fetch_add(d.ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
+        if (now == d.base + nblocks) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            __hip_atomic_store(d.flag, now, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
 
 // The footprint of a call's frames — 256 descriptors spread evenly over the call's tag & 0xFFFFFFFF
 // packets from desc (the whole call, also when it runs as sub-batches: the first sub-batch samples):
@@ -1149,25 +1167,14 @@ DEV void rows_body(const DescW<PW>& D, uint64_t pw, uint32_t n, uint8_t* arena, 
                                                                                  frame_stores, table_n, wmac, table);
 }
 
-// LAM: 0 frame-relative windows of K slots; 1 line-aligned windows of KL slots; 2 per wave, line-
-// aligned (KL slots) when a row of the wave starts mid-line, else frame-relative (K slots), so
-// line-aligned batches run the frame-relative code unchanged.
-template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM = 0, int KL = K>
-__global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
-                                                              uint32_t nblocks, uint8_t* __restrict__ arena,
-                                                              uint64_t arena_bytes, uint32_t base16,
-                                                              const uint32_t* __restrict__ nh,
-                                                              uint64_t* __restrict__ obs,
-                                                              uint8_t* __restrict__ status,
-                                                              nfcs_patch* __restrict__ patch,
-                                                              nfcs_patch* __restrict__ ws,
-                                                              const nfcs_nexthop* __restrict__ table,
-                                                              uint32_t table_n, uint64_t obs_tag) {
+// One wave of update_rows_kernel: its PW packets from the descriptor load on.
+template <int K, int R, int BS, bool FWD, int SF, int LAM, int KL>
+DEV void rows_wave(const nfcs_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                   uint32_t base16, const uint32_t* __restrict__ nh, uint64_t* __restrict__ obs,
+                   uint8_t* __restrict__ status, nfcs_patch* __restrict__ patch, nfcs_patch* __restrict__ ws,
+                   const nfcs_nexthop* __restrict__ table, uint32_t table_n, uint64_t obs_tag, uint32_t lane,
+                   uint32_t rl, uint32_t row, uint32_t rowbase4, uint64_t pw) {
     constexpr uint32_t PW = 64 / R;  // packets per wave
-    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
-    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
-    const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (BS / R) + rfl(threadIdx.x >> 6) * PW;
-    if (pw >= n) return;
     if (blockIdx.x == 0 && threadIdx.x < 64 && obs) sample_footprint(desc, obs_tag, lane, obs);
     // the wave's PW descriptors: one scalar load (s_load_dwordx8 for PW = 4)
     const DescW<PW> D = load_descw<PW>(desc, pw, n);
@@ -1214,6 +1221,32 @@ __global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* _
     else
         rows_body<K, R, BS, FWD, SF, false, PW>(D, pw, n, arena, arena_bytes, base16, rl, row, rowbase4, defer, q,
                                                 status, patch, ws, table, table_n);
+}
+
+// LAM: 0 frame-relative windows of K slots; 1 line-aligned windows of KL slots; 2 per wave, line-
+// aligned (KL slots) when a row of the wave starts mid-line, else frame-relative (K slots), so
+// line-aligned batches run the frame-relative code unchanged.
+template <int K, int R, int OCC, int BS, bool FWD, int SF, int LAM = 0, int KL = K>
+__global__ __launch_bounds__(BS, OCC) void update_rows_kernel(const nfcs_desc* __restrict__ desc, uint32_t n,
+                                                              uint32_t nblocks, uint8_t* __restrict__ arena,
+                                                              uint64_t arena_bytes, uint32_t base16,
+                                                              const uint32_t* __restrict__ nh,
+                                                              uint64_t* __restrict__ obs,
+                                                              uint8_t* __restrict__ status,
+                                                              nfcs_patch* __restrict__ patch,
+                                                              nfcs_patch* __restrict__ ws,
+                                                              const nfcs_nexthop* __restrict__ table,
+                                                              uint32_t table_n, uint64_t obs_tag, DoneReq done) {
+    constexpr uint32_t PW = 64 / R;  // packets per wave
+    const uint32_t lane = threadIdx.x & 63u, rl = lane & (R - 1), row = lane / R;
+    const uint32_t rowbase4 = (lane & ~(uint32_t)(R - 1)) * 4u;
+    const uint64_t pw = (uint64_t)xcd_block_n(nblocks) * (BS / R) + rfl(threadIdx.x >> 6) * PW;
+    // with a DoneReq (a kernel argument: uniform) waves without packets stay for signal_done's barrier
+    if (pw >= n && !done.flag) return;
+    if (pw < n)
+        rows_wave<K, R, BS, FWD, SF, LAM, KL>(desc, n, arena, arena_bytes, base16, nh, obs, status, patch, ws, table,
+                                              table_n, obs_tag, lane, rl, row, rowbase4, pw);
+    if (done.flag) signal_done(done, nblocks);
 }
 
 // SF_DEFER's write pass: the patch records of the waves that deferred, written into the frames
@@ -1363,15 +1396,15 @@ static void launch_rows(uint32_t grid, unsigned lds, hipStream_t stream, uint8_t
                         nfcs_patch* ws, const FwdArgs& fa) {
     hipLaunchKernelGGL((update_rows_kernel<K, R, OCC, BS, FWD, SF, LAM, KL>), dim3(grid), dim3(BS), lds, stream, desc, n, grid,
                        arena, arena_bytes, base16, fa.nh, fa.obs.slot, status, patch, ws, fa.table, fa.table_n,
-                       fa.obs.tag);
+                       fa.obs.tag, fa.done);
 }
 
 // One launch of the checksum path (its read pass and, for kUpdateAuto, its write pass) over n
 // packets, in the shape chosen for the whole call.
 static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const nfcs_desc* desc, uint32_t n,
                                     uint32_t base16, uint8_t* status, nfcs_patch* patch, nfcs_patch* ws,
-                                    int form, int shape, hipStream_t stream, ObsReq obs) {
-    const FwdArgs nofwd = {nullptr, nullptr, 0, obs};
+                                    int form, int shape, hipStream_t stream, ObsReq obs, DoneReq done = {}) {
+    const FwdArgs nofwd = {nullptr, nullptr, 0, obs, done};
     // a burst of at most kInlineMaxPackets packets: one kernel, every wave inline (the write pass's
     // launch would cost more than deferral saves on so few packets)
     if (form == kUpdateAuto && n <= kInlineMaxPackets) form = kUpdateInline;
@@ -1416,10 +1449,11 @@ static hipError_t launch_update_one(uint8_t* arena, uint64_t arena_bytes, const 
 hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,
                          const nfcs_desc* desc, uint32_t n, uint32_t base16, uint8_t* status,
                          nfcs_patch* patch, nfcs_patch* ws, int form, hipStream_t stream,
-                         uint64_t slot_bytes, ObsReq obs) {
+                         uint64_t slot_bytes, ObsReq obs, DoneReq done) {
     (void)di;
     if (n == 0) return hipSuccess;
     if (form == kUpdateRecords && !patch) return hipErrorInvalidValue;
+    if (done.flag && form == kUpdateAuto) return hipErrorInvalidValue;  // one kernel per call only
     if (form == kUpdateAuto && !patch && !ws) return hipErrorInvalidValue;
     // The short shape at 7 waves/SIMD: __launch_bounds__ 7 caps the kernel at 94 SGPRs (at the
     // compiler's 106 the SGPR file admits only 6 waves/SIMD: C3 +2%). Its workgroups were one wave
@@ -1449,7 +1483,7 @@ hipError_t launch_update(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes
         }
         return hipSuccess;
     }
-    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, shape, stream, obs);
+    return launch_update_one(arena, arena_bytes, desc, n, base16, status, patch, ws, form, shape, stream, obs, done);
 }
 
 hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes,

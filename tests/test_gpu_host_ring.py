@@ -231,3 +231,42 @@ def test_pageable_arena_at_any_address(engine, mode, shift):
     assert np.array_equal(view, ref)
     assert np.array_equal(big[:shift], guard[:shift])
     assert np.array_equal(big[shift + ring.nbytes:], guard[shift + ring.nbytes:])
+
+
+def test_bursts_of_every_size_in_sequence(engine):
+    """Round 6: host bursts small enough to run as direct chunks (no DMA; the kernel's last workgroup
+    signals through a host-mapped flag, nfcs::DoneReq) alternate with ones that take the copy engines,
+    through all three host entry points and both staging slots — 300 calls of 1 to 40,000 frames over a
+    pinned arena, a pageable one and scattered frames, each call's bytes and statuses the oracle's, so the
+    slots' completion counters and their event / flag waits stay in step across every kind of call."""
+    rng = np.random.default_rng(71)
+    frames = oracle.fuzz_frames(47, 0, 40_000)
+    arena, desc = oracle.pack_frames(frames)
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    pinned = engine.host_array(arena.nbytes)
+    try:
+        for k in range(300):
+            n = int(rng.choice([1, 3, 64, 256, 1000, 4000, 40_000], p=[.1, .1, .3, .2, .15, .1, .05]))
+            i = int(rng.integers(0, len(desc) - n + 1))
+            sub = np.ascontiguousarray(desc[i: i + n])
+            kind = k % 3
+            if kind == 0:
+                pinned[:] = arena
+                st = engine.update_host(pinned, sub)
+                got = pinned
+            elif kind == 1:
+                work = arena.copy()
+                st = engine.update_host(work, sub)
+                got = work
+            else:
+                buf = arena.copy()
+                offs = sub["off16"].astype(np.int64) * 16
+                st = engine.update_host_frames(buf, offs, sub["len"].astype(np.uint32))
+                got = buf
+            assert np.array_equal(st, rst[i: i + n]), (k, kind, n)
+            lo, hi = int(desc[i]["off16"]) * 16, int(desc[i + n - 1]["off16"]) * 16 + int(desc[i + n - 1]["len"])
+            assert np.array_equal(got[lo:hi], ref[lo:hi]), (k, kind, n)
+            assert np.array_equal(got[:lo], arena[:lo]) and np.array_equal(got[hi:], arena[hi:]), (k, kind, n)
+    finally:
+        engine.host_free(pinned)

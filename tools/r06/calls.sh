@@ -134,4 +134,21 @@ call_j() {
       > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
   done; done
 }
+
+call_k() {
+  # round 6, GPU call k: direct chunks signal completion through a host-mapped flag (nfcs::DoneReq) instead
+  # of the event: host-path GPU tests; host_lat; burstbench against the library before (zc = git f873852);
+  # the device lines C1 / C3 / forward C3 against it too (the kernel's early exit moved), alternating
+  local o=gpurun_out/r6k; mkdir -p $o
+  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_netflow_adapter.py \
+    tests/test_gpu_parity.py tests/test_gpu_large_arena.py tests/test_gpu_slot_hint.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 || return 1
+  timeout -k 10 120 tools/r06/host_lat > $o/host_lat.json 2> $o/host_lat.err || return 1
+  local r lib exe
+  for r in 1 2; do for lib in cur zc; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 64,256,1024,4096,16384,65536 1048576 0.4 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+  ab_lines $o 2 "cur zc" "c1 --steps 50" "c3 --config 3 --steps 40" "fwdc3 --op l3fwd --config 3 --steps 40"
+}
 "call_$1"
