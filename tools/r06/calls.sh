@@ -151,4 +151,11 @@ call_k() {
   done; done
   ab_lines $o 2 "cur zc" "c1 --steps 50" "c3 --config 3 --steps 40" "fwdc3 --op l3fwd --config 3 --steps 40"
 }
+
+call_l() {
+  # round 6, GPU call l: the completion-flag kernel change against git f873852 on the device lines it might
+  # move (the forward's C3 mix, C1), four alternating rounds
+  local o=gpurun_out/r6l; mkdir -p $o
+  ab_lines $o 4 "cur zc" "fwdc3 --op l3fwd --config 3 --steps 40" "c1 --steps 50"
+}
 "call_$1"
