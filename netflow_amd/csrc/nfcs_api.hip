@@ -357,6 +357,21 @@ constexpr uint64_t kDirectChunkBytes = NFCS_DIRECT_CHUNK_BYTES;
 #define NFCS_ZERO_COPY_AUTO_BYTES (32u << 20)
 #endif
 constexpr uint64_t kZeroCopyAutoBytes = NFCS_ZERO_COPY_AUTO_BYTES;
+// The staged chunk size of a host burst of `total` bytes: about total / kChunksPerBurst (at least
+// kMinChunkBytes, at most a staging slot), so that the host copies, the transfers, the kernel and the
+// write-back of successive chunks overlap across the two slots even when the burst would fit one slot
+// (round 2: 16K C1 frames pinned 583 -> 559 µs, pageable 979 -> 710 µs in 4 chunks of >= 4 MiB).
+#ifndef NFCS_MIN_CHUNK_BYTES
+#define NFCS_MIN_CHUNK_BYTES (4ull << 20)
+#endif
+#ifndef NFCS_CHUNKS_PER_BURST
+#define NFCS_CHUNKS_PER_BURST 4
+#endif
+constexpr uint64_t kMinChunkBytes = NFCS_MIN_CHUNK_BYTES;
+constexpr uint64_t kChunksPerBurst = NFCS_CHUNKS_PER_BURST;
+inline uint64_t chunk_bytes(uint64_t total) {
+    return std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max<uint64_t>(kMinChunkBytes, total / kChunksPerBurst));
+}
 // Host copy work per thread before a copy is split over the workers (a worker's wake-up costs ~10 µs;
 // one thread stages ~15 GB/s): gathers and staging copies from 512 KiB, write-backs from 2048 frames.
 constexpr uint64_t kCopyBytesPerThread = 512u << 10;
@@ -953,10 +968,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     // two slots even when it would fit one slot (16K C1 frames: pinned 583 -> 559 µs, pageable
     // 979 -> 710 µs; 64K: 2267 -> 1992 / 3133 -> 2273 µs). Whole frames back from a pinned arena
     // keep slot-sized chunks (4 chunks measured slower there: 64K 3.13 -> 3.59 ms).
-    constexpr uint64_t kMinChunk = 4ull << 20;
-    const uint64_t chunk_target = (!patch_only && pinned)
-                                      ? nfcs_ctx::kStageBytes
-                                      : std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max(kMinChunk, span / 4));
+    const uint64_t chunk_target = (!patch_only && pinned) ? nfcs_ctx::kStageBytes : chunk_bytes(span);
 
     struct Chunk { uint32_t i0, i1; uint64_t base, bytes; bool used; };
     Chunk slot[nfcs_ctx::kSlots] = {};
@@ -1156,8 +1168,7 @@ NFCS_API int nfcs_update_host_frames(nfcs_ctx* c, uint8_t* const* frames, const 
         }
         // chunks of ~a quarter of the burst (at least 4 MiB, at most a staging slot), as
         // nfcs_update_host cuts them
-        constexpr uint64_t kMinChunk = 4ull << 20;
-        chunk_target = std::min<uint64_t>(nfcs_ctx::kStageBytes, std::max(kMinChunk, total / 4));
+        chunk_target = chunk_bytes(total);
     }
 
     // The pipeline over the two slots, per chunk k in slot s: wait until chunk k-2's frames and

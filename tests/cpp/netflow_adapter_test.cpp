@@ -805,7 +805,9 @@ private:
 //                PacketBuffer objects (one `new[]` each; nfcs_update_host_frames: gather, H2D, GPU,
 //                checksum bytes written back);
 //   pinned_ring  nfcs_update_host over the same frames in one pinned arena, 1536-byte slots (a NIC
-//                ring's DMA area; frames H2D, patch records back);
+//                ring's DMA area; zero-copy up to 32 MiB, frames H2D and patch records back above), its
+//                NFCS_HOST_ZERO_COPY form, and pageable_ring: the same ring in pageable memory (staged
+//                by the copy threads);
 //   reference_1_thread / reference_threads  the reference's per-packet Packet::update_checksums() over
 //                the burst's PacketBuffers, on one thread (the switch's own loop, switch.hpp:213-294) and
 //                on `threads` threads (a SpinPool).
@@ -839,6 +841,7 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
     std::vector<uint8_t> pristine(bytes);
     if (nfcs_memcpy_d2h(c, pristine.data(), d_arena, bytes)) return 1;
     uint8_t* pr = static_cast<uint8_t*>(h_ring);
+    std::vector<uint8_t> pageable(bytes);  // the same ring in pageable memory (staged by the copy threads)
     SpinPool copier(std::max<size_t>(1, std::min<size_t>(threads, 8)));  // restores and digests only, untimed
 
     std::vector<std::unique_ptr<netflow::PacketBuffer>> rb(n);
@@ -850,23 +853,25 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
         ptrs[i] = rp[i].get();
     }
     auto frame = [&](size_t i) -> const uint8_t* { return pristine.data() + (size_t)desc[i].off16 * 16; };
-    auto restore = [&](bool ring_arena) {
+    // arena kinds: 0 the reference's PacketBuffers, 1 the pinned ring, 2 the pageable ring
+    auto ring_of = [&](int kind) { return kind == 1 ? pr : pageable.data(); };
+    auto restore = [&](int kind) {
         copier.run(n, [&](size_t i0, size_t i1) {
             for (size_t i = i0; i < i1; ++i) {
-                uint8_t* d = ring_arena ? pr + (size_t)desc[i].off16 * 16 : rb[i]->get_data_start_ptr();
+                uint8_t* d = kind ? ring_of(kind) + (size_t)desc[i].off16 * 16 : rb[i]->get_data_start_ptr();
                 std::memcpy(d, frame(i), desc[i].len);
             }
         });
     };
     std::vector<uint8_t> img(bytes);
-    auto digest = [&](bool ring_arena) -> std::string {
-        if (!ring_arena)
+    auto digest = [&](int kind) -> std::string {
+        if (!kind)
             copier.run(n, [&](size_t i0, size_t i1) {
                 for (size_t i = i0; i < i1; ++i)
                     std::memcpy(img.data() + (size_t)desc[i].off16 * 16, rb[i]->get_data_start_ptr(), desc[i].len);
             });
         uint64_t d = 0;
-        if (nfcs_memcpy_h2d(c, d_arena, ring_arena ? pr : img.data(), bytes) ||
+        if (nfcs_memcpy_h2d(c, d_arena, kind ? ring_of(kind) : img.data(), bytes) ||
             nfcs_digest_device(c, (uint8_t*)d_arena, bytes, (nfcs_desc*)d_desc, (uint32_t)n, 0, &d, nullptr))
             return "error";
         char s[32];
@@ -878,9 +883,9 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
     // one path: call(off, b) checksums packets [off, off + b) of the ring
     std::string out;
     bool all_match = true;
-    auto path = [&](const char* name, bool ring_arena, const std::function<int(size_t, size_t)>& call) -> int {
+    auto path = [&](const char* name, int kind, const std::function<int(size_t, size_t)>& call) -> int {
         std::fprintf(stderr, "burstbench: %s\n", name);
-        restore(ring_arena);
+        restore(kind);
         std::string legs;
         for (size_t b : sizes) {
             if (b == 0 || n % b) return NFCS_EINVAL;
@@ -908,7 +913,7 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
             const int r = call(k * big, big);
             if (r) return r;
         }
-        const std::string d = digest(ring_arena);
+        const std::string d = digest(kind);
         all_match = all_match && d == want;
         char o[160];
         std::snprintf(o, sizeof(o), "}, \"digest\": \"%s\", \"match\": %s}", d.c_str(), d == want ? "true" : "false");
@@ -916,23 +921,27 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
         return NFCS_OK;
     };
 
-    rc = path("adapter", false, [&](size_t off, size_t b) { return netflow_amd::update_checksums_batch(ptrs.data() + off, b); });
+    rc = path("adapter", 0, [&](size_t off, size_t b) { return netflow_amd::update_checksums_batch(ptrs.data() + off, b); });
     if (!rc)
-        rc = path("pinned_ring", true, [&](size_t off, size_t b) {
+        rc = path("pinned_ring", 1, [&](size_t off, size_t b) {
             return nfcs_update_host(c, pr, bytes, desc.data() + off, (uint32_t)b, nullptr, 0);
         });
     if (!rc)
-        rc = path("pinned_ring_zero_copy", true, [&](size_t off, size_t b) {
+        rc = path("pinned_ring_zero_copy", 1, [&](size_t off, size_t b) {
             return nfcs_update_host(c, pr, bytes, desc.data() + off, (uint32_t)b, nullptr, NFCS_HOST_ZERO_COPY);
         });
     if (!rc)
-        rc = path("reference_1_thread", false, [&](size_t off, size_t b) {
+        rc = path("pageable_ring", 2, [&](size_t off, size_t b) {
+            return nfcs_update_host(c, pageable.data(), bytes, desc.data() + off, (uint32_t)b, nullptr, 0);
+        });
+    if (!rc)
+        rc = path("reference_1_thread", 0, [&](size_t off, size_t b) {
             for (size_t i = off; i < off + b; ++i) ptrs[i]->update_checksums();
             return 0;
         });
     if (!rc) {
         SpinPool pool(threads);
-        rc = path("reference_threads", false, [&](size_t off, size_t b) {
+        rc = path("reference_threads", 0, [&](size_t off, size_t b) {
             pool.run(b, [&](size_t i0, size_t i1) { for (size_t i = off + i0; i < off + i1; ++i) ptrs[i]->update_checksums(); });
             return 0;
         });

@@ -158,4 +158,26 @@ call_l() {
   local o=gpurun_out/r6l; mkdir -p $o
   ab_lines $o 4 "cur zc" "fwdc3 --op l3fwd --config 3 --steps 40" "c1 --steps 50"
 }
+
+call_m() {
+  # round 6, GPU call m: every GPU test on the product after the host-path changes, then the default bench
+  # line (the driver's command) and smoke()
+  local o=gpurun_out/r6m; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 || return 1
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || return 1
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
+
+call_n() {
+  # round 6, GPU call n: host chunk sizes for mid-size bursts — the product (chunks of >= 4 MiB, ~4 per
+  # burst) against >= 2 MiB / 1 MiB / 512 KiB chunks, ~8 per burst (tools/r06/build_variant.sh), burstbench
+  # with the pageable ring, alternating, two rounds
+  local o=gpurun_out/r6n; mkdir -p $o
+  local r lib exe
+  for r in 1 2; do for lib in cur ch2m8 ch1m8 ch512k8; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 256,1024,4096,16384,65536 1048576 0.3 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+}
 "call_$1"
