@@ -695,15 +695,16 @@ struct FwdArgs {
     DoneReq done = {};
 };
 
-// DoneReq (nfcs_internal.h): every wave of the workgroup has issued its stores (the barrier); one lane
-// releases them at system scope and counts the workgroup (a vector atomic); the workgroup that completes
-// the count publishes it with a system-scope release store (a vector store), which the host's acquire
-// load of the flag pairs with. Waves that had no packets reach the barrier too (update_rows_kernel
-// returns early only without a DoneReq).
+// DoneReq (nfcs_internal.h): every wave releases its own frame / record / status stores at system scope
+// (each wave's fence waits for that wave's stores; one lane's fence would not cover the other waves'
+// stores still in flight), the barrier then has them all; one lane counts the workgroup (a vector
+// atomic), and the workgroup that completes the count publishes it with a system-scope release store
+// (a vector store), which the host's acquire load of the flag pairs with. Waves that had no packets reach
+// the barrier too (update_rows_kernel returns early only without a DoneReq).
 DEV void signal_done(const DoneReq& d, uint32_t nblocks) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this workgroup's frame / record stores
         const uint64_t now = __hip_atomic_fetch_add(d.ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
         if (now == d.base + nblocks) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");

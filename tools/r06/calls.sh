@@ -180,4 +180,15 @@ call_n() {
       > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
   done; done
 }
+
+call_o() {
+  # round 6, GPU call o: every wave releases its own stores before signal_done's barrier (instead of lane 0
+  # of the workgroup alone): the host-path and slot tests, host_lat, burstbench
+  local o=gpurun_out/r6o; mkdir -p $o
+  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_netflow_adapter.py \
+    tests/test_gpu_parity.py tests/test_gpu_slot_hint.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 || return 1
+  timeout -k 10 120 tools/r06/host_lat > $o/host_lat.json 2> $o/host_lat.err || return 1
+  timeout -k 10 300 tests/cpp/_ref/netflow_adapter_test burstbench 64,256,1024,4096,16384,65536 1048576 0.3 16 81cc3905092d7f44 \
+      > $o/burst_cur_1.json 2> $o/burst_cur_1.err
+}
 "call_$1"
