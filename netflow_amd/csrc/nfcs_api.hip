@@ -374,7 +374,10 @@ inline uint64_t chunk_bytes(uint64_t total) {
 }
 // Host copy work per thread before a copy is split over the workers (a worker's wake-up costs ~10 µs;
 // one thread stages ~15 GB/s): gathers and staging copies from 512 KiB, write-backs from 2048 frames.
-constexpr uint64_t kCopyBytesPerThread = 512u << 10;
+#ifndef NFCS_COPY_BYTES_PER_THREAD
+#define NFCS_COPY_BYTES_PER_THREAD (512u << 10)
+#endif
+constexpr uint64_t kCopyBytesPerThread = NFCS_COPY_BYTES_PER_THREAD;
 constexpr uint32_t kPatchFramesPerThread = 2048;
 
 // Host copies whose destination this CPU does not read again (the staging slots, which the copy

@@ -191,4 +191,16 @@ call_o() {
   timeout -k 10 300 tests/cpp/_ref/netflow_adapter_test burstbench 64,256,1024,4096,16384,65536 1048576 0.3 16 81cc3905092d7f44 \
       > $o/burst_cur_1.json 2> $o/burst_cur_1.err
 }
+
+call_p() {
+  # round 6, GPU call p: host copy split per thread from 512 KiB (product) against 256 / 128 KiB, burstbench
+  # alternating, two rounds
+  local o=gpurun_out/r6p; mkdir -p $o
+  local r lib exe
+  for r in 1 2; do for lib in cur cp256k cp128k; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 64,256,1024,4096,16384 1048576 0.3 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+}
 "call_$1"
