@@ -177,8 +177,10 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
  * chunks on two streams (from a pageable arena through the context's pinned ring, copied by host
  * threads; a pinned arena — nfcs_host_alloc — is copied from directly), the kernel runs per
  * chunk, and only the 8-byte nfcs_patch records come back and are applied on the host. A frame
- * inside the arena larger than one staging slot (64 MiB) is NFCS_EINVAL, checked before anything
- * is queued.
+ * inside the arena longer than NFCS_FRAME_RELEVANT_BYTES is staged as its first
+ * NFCS_FRAME_RELEVANT_BYTES bytes, with the same result (see nfcs_update_host_frames); before round 6
+ * a frame larger than one 64 MiB staging slot was NFCS_EINVAL. Pinned bursts of up to 32 MiB run
+ * zero-copy (below).
  * flags:
  *   NFCS_HOST_FRAMES     copy whole frames back instead of patch records (same bytes, slower;
  *                        each chunk's span goes back whole, so bytes between the burst's frames

@@ -599,13 +599,33 @@ bool is_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
+// A caller's descriptor as the host path stages it: a frame inside the arena that is longer than
+// kFrameRelevantBytes goes as its first kFrameRelevantBytes — the same result (nfcs.h), and no frame
+// outgrows a staging slot; others unchanged (a frame reaching past the arena stays NFCS_ST_BAD_DESC).
+inline nfcs_desc staged_desc(const nfcs_desc& d, uint64_t arena_bytes) {
+    const uint64_t o = (uint64_t)d.off16 * 16u;
+    if (d.len > nfcs::kFrameRelevantBytes && o + (((uint64_t)d.len + 15u) & ~15ull) <= arena_bytes)
+        return nfcs_desc{d.off16, nfcs::kFrameRelevantBytes};
+    return d;
+}
+// Descriptors [i, i + m) into a staging slot, as staged_desc stages them (a plain copy when the burst
+// has no frame longer than kFrameRelevantBytes).
+void stage_descs(nfcs_desc* dst, const nfcs_desc* src, uint32_t m, uint64_t arena_bytes, bool any_long) {
+    if (!any_long) {
+        memcpy(dst, src, (size_t)m * sizeof(nfcs_desc));
+        return;
+    }
+    for (uint32_t j = 0; j < m; ++j) dst[j] = staged_desc(src[j], arena_bytes);
+}
+
 // The arena bytes that descriptors [i0, i1) span, summed over their runs of ascending offsets: a NIC
 // ring burst that wraps past the ring's end is two runs, each from its first frame's start to the end
 // of its furthest frame (frames outside the arena count nothing). The launch shape's footprint.
 uint64_t run_span(const nfcs_desc* d, uint32_t i0, uint32_t i1, uint64_t arena_bytes) {
     uint64_t total = 0, lo = 0, hi = 0;
     for (uint32_t i = i0; i < i1; ++i) {
-        const uint64_t o = (uint64_t)d[i].off16 * 16u, e = o + (((uint64_t)d[i].len + 15u) & ~15ull);
+        const nfcs_desc sd = staged_desc(d[i], arena_bytes);
+        const uint64_t o = (uint64_t)sd.off16 * 16u, e = o + (((uint64_t)sd.len + 15u) & ~15ull);
         if (i == i0 || d[i].off16 < d[i - 1].off16) {  // a new run
             total += hi - lo;
             lo = hi = std::min(o, arena_bytes);
@@ -624,7 +644,7 @@ uint64_t run_span(const nfcs_desc* d, uint32_t i0, uint32_t i1, uint64_t arena_b
 // slots are drained before returning, so nothing is left in flight on the caller's memory. Also the
 // default form of nfcs_update_host for pinned bursts of up to kZeroCopyAutoBytes.
 int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
-                          const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status) {
+                          const nfcs_desc* h_desc, uint32_t n, uint8_t* h_status, bool any_long) {
     void* dptr = nullptr;
     NFCS_HIP(hipHostGetDevicePointer(&dptr, h_arena, 0));
     uint8_t* d_arena = static_cast<uint8_t*>(dptr);
@@ -644,7 +664,7 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
         if (e != hipSuccess) break;
         const uint32_t m = std::min<uint32_t>(n - i, c->stage_pkts);
         hipStream_t st = c->hs[s];
-        memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        stage_descs(c->h_desc[s], h_desc + i, m, arena_bytes, any_long);
         // the launch shape follows this chunk's own frames (their span per packet, over the runs of
         // a burst that wraps its ring), not the caller's whole arena, unless the context has a hint
         const uint64_t span = run_span(h_desc, i, i + m, arena_bytes);
@@ -931,21 +951,23 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     if (dg_.err != hipSuccess) return hip_fail(dg_.err);
     if (n == 0) return NFCS_OK;
     if (!h_arena || !h_desc) return NFCS_EINVAL;
-    // Checked before anything is queued: every frame that lies inside the arena fits one staging
-    // slot. A frame reaching past the arena is staged as nothing and becomes NFCS_ST_BAD_DESC (the
+    // Every frame inside the arena fits one staging slot as staged (staged_desc: a frame longer than
+    // kFrameRelevantBytes goes as its first kFrameRelevantBytes, round 6; NFCS_EINVAL above 64 MiB
+    // before). A frame reaching past the arena is staged as nothing and becomes NFCS_ST_BAD_DESC (the
     // kernel checks it against its chunk), as on the device path. Frames come in any order: a chunk
     // is a run of ascending offsets, so a burst that wraps past its ring's end (round 5; VERDICT r4
     // item 4) is split where an offset drops below its predecessor's, as separate PacketBuffers
     // (packet_buffer.hpp:21-31) never constrain their order either.
-    auto frame_end = [&](uint32_t i) -> uint64_t {  // 0: outside the arena
-        const uint64_t o = (uint64_t)h_desc[i].off16 * 16u;
-        const uint64_t e = o + (((uint64_t)h_desc[i].len + 15u) & ~15ull);
+    auto frame_end = [&](uint32_t i) -> uint64_t {  // 0: outside the arena; as staged (staged_desc)
+        const nfcs_desc d = staged_desc(h_desc[i], arena_bytes);
+        const uint64_t o = (uint64_t)d.off16 * 16u;
+        const uint64_t e = o + (((uint64_t)d.len + 15u) & ~15ull);
         return e <= arena_bytes ? e : 0;
     };
     bool ordered = true;  // ascending offsets: the chunks' spans are disjoint
+    bool any_long = false;  // a frame inside the arena longer than kFrameRelevantBytes (staged_desc)
     for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t e = frame_end(i);
-        if (e && e - (uint64_t)h_desc[i].off16 * 16u > nfcs_ctx::kStageBytes) return NFCS_EINVAL;
+        any_long = any_long || h_desc[i].len > nfcs::kFrameRelevantBytes;
         ordered = ordered && (i == 0 || h_desc[i].off16 >= h_desc[i - 1].off16);
     }
     const uint64_t span = run_span(h_desc, 0, n, arena_bytes);
@@ -954,14 +976,14 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     const bool pinned = is_pinned(h_arena);
     if (flags & NFCS_HOST_ZERO_COPY) {
         if (!pinned) return NFCS_EINVAL;
-        return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status);
+        return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status, any_long);
     }
     // A pinned arena's burst of at most kZeroCopyAutoBytes of frames (the default, records form) runs
     // zero-copy: the kernel reads its frames in place and stores the checksum bytes straight back,
     // the same bytes the records would carry (round 6, profiles/r06_host_bursts_ab.jsonl: 64 to 16K C1
     // frames 2-18% faster zero-copy than through the copy engines, 64K 3-5% slower)
     if (pinned && !(flags & NFCS_HOST_FRAMES) && span <= kZeroCopyAutoBytes)
-        return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status);
+        return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status, any_long);
     // default: frames H2D and only the 8-byte patch records D2H (kUpdateRecords: the staged
     // frames are not written), applied here; whole frames back only on request (NFCS_HOST_FRAMES:
     // kUpdateAuto on the staged frames, the slot's patch buffer as the deferred-store workspace)
@@ -1021,7 +1043,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
                     const uint32_t q = k.i0 + j;
                     if (!frame_end(q)) continue;
                     const uint64_t o = (uint64_t)h_desc[q].off16 * 16u;
-                    memcpy(h_arena + o, c->h_arena[s] + (o - k.base), h_desc[q].len);
+                    memcpy(h_arena + o, c->h_arena[s] + (o - k.base), staged_desc(h_desc[q], arena_bytes).len);
                 }
             });
         }
@@ -1073,7 +1095,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
             par_memcpy(c, c->h_arena[s], src, bytes);
             src = c->h_arena[s];
         }
-        memcpy(c->h_desc[s], h_desc + i, (size_t)m * sizeof(nfcs_desc));
+        stage_descs(c->h_desc[s], h_desc + i, m, arena_bytes, any_long);
         if (patch_only) {
             finish(s);  // chunk k-2's records and statuses are read out before chunk k's land
             if (e != hipSuccess) break;

@@ -256,17 +256,28 @@ def test_host_path_out_of_arena_descriptors_multi_chunk(engine, mode):
     assert np.array_equal(arena, ref)
 
 
-def test_host_path_frame_larger_than_a_slot_is_rejected_untouched(engine):
-    """A frame inside the arena but larger than a 64 MiB staging slot cannot be staged: the call
-    returns NFCS_EINVAL before anything is queued, and the arena is unchanged."""
-    arena, desc = oracle.gen_config(1, SEED, 0, 1000)
-    big = np.zeros((65 << 20) + 4096, np.uint8)
-    big[: arena.nbytes] = arena
-    desc = desc.copy()
-    desc[500]["len"] = 65 << 20
-    desc[500]["off16"] = 0  # keeps arena order only with the frames before it moved too
-    desc = desc[500:]
-    before = big.copy()
-    with pytest.raises(nf.NfcsError):
-        engine.update_host(big, desc)
-    assert np.array_equal(big, before)
+@pytest.mark.parametrize("mode", ["patch", "frames", "pinned", "zero_copy"])
+def test_host_path_frame_larger_than_a_slot(engine, mode):
+    """A frame inside the arena longer than a 64 MiB staging slot (round 6; NFCS_EINVAL before): it is
+    staged as its first NFCS_FRAME_RELEVANT_BYTES, which gives the same bytes — the reference reads and
+    bounds-tests no offset past 65,613 — so the whole arena, the frames around it and the frame's own
+    65 MiB tail equal the oracle's update of the whole frames, in every host mode."""
+    arena0, desc0 = oracle.gen_config(1, SEED, 0, 1000)
+    frames = oracle.unpack_frames(arena0, desc0)
+    rng = np.random.default_rng(5)
+    huge = frames[500] + rng.integers(0, 256, (65 << 20) - len(frames[500]), dtype=np.uint8).tobytes()
+    arena, desc = oracle.pack_frames(frames[:500] + [huge] + frames[500:])
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    if mode in ("pinned", "zero_copy"):
+        host = engine.host_array(arena.nbytes)
+        host[:] = arena
+    else:
+        host = arena
+    try:
+        st = engine.update_host(host, desc, mode={"pinned": "patch"}.get(mode, mode))
+        assert np.array_equal(st, rst)
+        assert np.array_equal(host, ref)
+    finally:
+        if host is not arena:
+            engine.host_free(host)

@@ -203,4 +203,12 @@ call_p() {
       > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
   done; done
 }
+
+call_q() {
+  # round 6, GPU call q: frames longer than a staging slot in the arena host path (staged as their relevant
+  # prefix): the host-path GPU tests
+  local o=gpurun_out/r6q; mkdir -p $o
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py \
+    tests/test_netflow_adapter.py tests/test_gpu_large_arena.py -q -x --timeout 280 --timeout-method thread > $o/pytest.log 2>&1
+}
 "call_$1"
