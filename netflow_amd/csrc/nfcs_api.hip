@@ -982,7 +982,9 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
     // zero-copy: the kernel reads its frames in place and stores the checksum bytes straight back,
     // the same bytes the records would carry (round 6, profiles/r06_host_bursts_ab.jsonl: 64 to 16K C1
     // frames 2-18% faster zero-copy than through the copy engines, 64K 3-5% slower)
-    if (pinned && !(flags & NFCS_HOST_FRAMES) && span <= kZeroCopyAutoBytes)
+    // (a 16-byte aligned arena only: the kernel's 16-byte loads address the frames in place)
+    const bool aligned = ((uintptr_t)h_arena & 15u) == 0;
+    if (pinned && aligned && !(flags & NFCS_HOST_FRAMES) && span <= kZeroCopyAutoBytes)
         return update_host_zero_copy(c, h_arena, arena_bytes, h_desc, n, h_status, any_long);
     // default: frames H2D and only the 8-byte patch records D2H (kUpdateRecords: the staged
     // frames are not written), applied here; whole frames back only on request (NFCS_HOST_FRAMES:
@@ -1082,7 +1084,7 @@ NFCS_API int nfcs_update_host(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_byte
         const uint8_t* src = h_arena + base;
         // a direct chunk (records back, small): no DMA; the kernel reads a pinned arena in place
         uint8_t* zsrc = nullptr;
-        if (patch_only && c->z_block[s] && bytes <= kDirectChunkBytes) {
+        if (patch_only && c->z_block[s] && bytes <= kDirectChunkBytes && (!pinned || aligned)) {
             if (pinned) {
                 void* dp = nullptr;
                 if (hipHostGetDevicePointer(&dp, h_arena, 0) == hipSuccess) zsrc = static_cast<uint8_t*>(dp) + base;

@@ -270,3 +270,32 @@ def test_bursts_of_every_size_in_sequence(engine):
             assert np.array_equal(got[:lo], arena[:lo]) and np.array_equal(got[hi:], arena[hi:]), (k, kind, n)
     finally:
         engine.host_free(pinned)
+
+
+@pytest.mark.parametrize("shift", [16, 4096, 1 << 20, 8, 3])
+def test_pinned_arena_at_an_interior_address(engine, shift):
+    """Round 6: a pinned burst of up to 32 MiB runs zero-copy by default, the kernel addressing the
+    caller's arena through hipHostGetDevicePointer — here an arena that starts inside a pinned
+    allocation (a slice of a pinned ring, as a NIC driver hands out), small bursts (direct, completion
+    by flag) and one above 2 MiB; bytes and statuses the oracle's, the bytes before the arena untouched.
+    An arena that is not 16-byte aligned (shift 8, 3) is staged through the copy engines instead."""
+    frames = oracle.fuzz_frames(48, 0, 6000)
+    arena, desc = oracle.pack_frames(frames)
+    ref = arena.copy()
+    rst, _ = oracle.update_batch(ref, desc, nthreads=8)
+    pinned = engine.host_array(arena.nbytes + shift)
+    try:
+        junk = np.random.default_rng(shift).integers(0, 256, shift, dtype=np.uint8)
+        for lo, hi in ((0, 3), (100, 164), (0, len(desc))):
+            pinned[:shift] = junk
+            view = pinned[shift:]
+            view[:] = arena
+            sub = np.ascontiguousarray(desc[lo:hi])
+            st = engine.update_host(view, sub)
+            assert np.array_equal(st, rst[lo:hi]), (lo, hi)
+            a = int(desc[lo]["off16"]) * 16
+            b = int(desc[hi - 1]["off16"]) * 16 + int(desc[hi - 1]["len"])
+            assert np.array_equal(view[a:b], ref[a:b]), (lo, hi)
+            assert np.array_equal(pinned[:shift], junk)
+    finally:
+        engine.host_free(pinned)

@@ -211,4 +211,30 @@ call_q() {
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py \
     tests/test_netflow_adapter.py tests/test_gpu_large_arena.py -q -x --timeout 280 --timeout-method thread > $o/pytest.log 2>&1
 }
+
+call_r() {
+  # round 6, GPU call r: where the forward's long-frame read pass loses 4% to the update's (C1, deferred
+  # forms: update_rows_kernel<6,16,1,256,false,SF_DEFER,1,7> vs <6,16,7,256,true,SF_DEFER,2,7>): issue and
+  # stall counters and fetched bytes per dispatch, both ops on C1
+  local o=gpurun_out/r6r
+  PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD;FETCH_SIZE;SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" \
+    bash tools/pmc.sh r6r/pmc_fwd_c1 --op l3fwd --steps 20 --no-host --no-c4 --no-replay && \
+  PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD;FETCH_SIZE;SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" \
+    bash tools/pmc.sh r6r/pmc_upd_c1 --steps 20 --no-host --no-c4 --no-replay && \
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$o/prof_fwd_c1" -o p -- \
+    python3 bench.py --op l3fwd --steps 30 --no-cpu > $o/prof_fwd_c1.json 2> $o/prof_fwd_c1.err
+}
+
+call_s() {
+  # round 6, GPU call s: the round's evidence on the final kernels (tools/r06/prof_all.sh)
+  bash tools/r06/prof_all.sh r6s
+}
+
+call_t() {
+  # round 6, GPU call t: pinned arenas at interior / unaligned addresses (zero-copy by default only when
+  # 16-byte aligned): the host-path GPU tests
+  local o=gpurun_out/r6t; mkdir -p $o
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_gpu_parity.py \
+    -q -x --timeout 280 --timeout-method thread > $o/pytest.log 2>&1
+}
 "call_$1"
