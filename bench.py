@@ -1169,7 +1169,7 @@ def host_bursts_line(ring: int, sizes=BURST_SIZES, seconds: float = 0.25):
                          < out[ref]["bursts"][str(b)]["us_per_call"]), None)
         except KeyError:
             return None
-    gpu_paths = ("adapter", "pinned_ring", "pinned_ring_zero_copy", "pageable_ring")
+    gpu_paths = ("adapter", "pinned_ring", "pinned_ring_zero_copy", "pageable_ring", "buffer_pool")
     out["crossover_vs_reference_1_thread"] = {p: crossover(p, "reference_1_thread") for p in gpu_paths}
     out["crossover_vs_reference_threads"] = {p: crossover(p, "reference_threads") for p in gpu_paths}
     out["workload"] = (f"C1 frames (1500 B IPv4+UDP) in a ring of {human(ring)}, checksummed in consecutive bursts "

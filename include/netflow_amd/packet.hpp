@@ -652,16 +652,27 @@ inline int BufferPool::update_checksums_batch(Packet* const* pkts, size_t n, uin
     });
     if (foreign.load()) return eng_.update_checksums_batch(pkts, n, status);
     size_t drops = 0;  // places where the burst's arena offsets go down (a wrap of the pool's slots)
-    uint64_t frame_bytes = 0;
+    uint64_t frame_bytes = 0, span = 0, lo = 0, hi = 0;  // span: the runs' bytes, as nfcs_update_host stages them
     for (size_t i = 0; i < n; ++i) {
-        drops += i && desc[i].off16 < desc[i - 1].off16;
+        const uint64_t o = (uint64_t)desc[i].off16 * 16, e = o + ((desc[i].len + 15u) & ~15u);
+        if (i && desc[i].off16 < desc[i - 1].off16) {
+            ++drops;
+            span += hi - lo;
+            lo = hi = o;
+        } else if (i == 0) {
+            lo = hi = o;
+        }
+        hi = std::max(hi, e);
         frame_bytes += desc[i].len;
     }
+    span += hi - lo;
     // Frames that fill less than 85% of their slots: DMA'd as spans, the slots' unused bytes would
     // cross PCIe too (C1's 1500-byte frames in 2176-byte slots: 33 GB/s of frames); gathered by the
     // library's copy threads first, only frame bytes do (49 GB/s; round 5, profiles/r05_b_adapter_t8.json).
-    // NFCS_HOST_ZERO_COPY stays a span read in place.
-    if (flags == 0 && frame_bytes < n * slot_bytes_ * 85 / 100) {
+    // A burst spanning at most NFCS_HOST_ZERO_COPY_AUTO_BYTES runs zero-copy in nfcs_update_host, where the
+    // kernel reads only the frames' bytes in place: no gather then (round 6). NFCS_HOST_ZERO_COPY stays a
+    // span read in place.
+    if (flags == 0 && frame_bytes < n * slot_bytes_ * 85 / 100 && span > NFCS_HOST_ZERO_COPY_AUTO_BYTES) {
         std::vector<uint8_t*> fr(n);
         std::vector<uint32_t> ln(n);
         for (size_t i = 0; i < n; ++i) {

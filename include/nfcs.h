@@ -191,6 +191,10 @@ NFCS_API int nfcs_update_device(nfcs_ctx* ctx, uint8_t* d_arena, uint64_t arena_
  *                        form for pinned bursts of up to 32 MiB (round 6: one launch, no DMA)
  *   NFCS_HOST_PATCH_ONLY the default since ABI 1 session 2; accepted and ignored
  * Rates: DESIGN.md §7. */
+/* A pinned burst whose frames (its runs of ascending offsets, gaps included) span at most this many bytes
+ * runs zero-copy unless NFCS_HOST_FRAMES is given (round 6): one kernel launch and no DMA, the kernel
+ * reading only the frames' own bytes; larger bursts go through the copy engines. */
+#define NFCS_HOST_ZERO_COPY_AUTO_BYTES (32u << 20)
 #define NFCS_HOST_PATCH_ONLY 1u
 #define NFCS_HOST_ZERO_COPY 2u
 #define NFCS_HOST_FRAMES 4u

@@ -353,10 +353,7 @@ T* zdev(const nfcs_ctx* c, int s, T* host) {
 #define NFCS_DIRECT_CHUNK_BYTES (2u << 20)
 #endif
 constexpr uint64_t kDirectChunkBytes = NFCS_DIRECT_CHUNK_BYTES;
-#ifndef NFCS_ZERO_COPY_AUTO_BYTES
-#define NFCS_ZERO_COPY_AUTO_BYTES (32u << 20)
-#endif
-constexpr uint64_t kZeroCopyAutoBytes = NFCS_ZERO_COPY_AUTO_BYTES;
+constexpr uint64_t kZeroCopyAutoBytes = NFCS_HOST_ZERO_COPY_AUTO_BYTES;  // nfcs.h
 // The staged chunk size of a host burst of `total` bytes: about total / kChunksPerBurst (at least
 // kMinChunkBytes, at most a staging slot), so that the host copies, the transfers, the kernel and the
 // write-back of successive chunks overlap across the two slots even when the burst would fit one slot

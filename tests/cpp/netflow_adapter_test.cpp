@@ -808,6 +808,8 @@ private:
 //                ring's DMA area; zero-copy up to 32 MiB, frames H2D and patch records back above), its
 //                NFCS_HOST_ZERO_COPY form, and pageable_ring: the same ring in pageable memory (staged
 //                by the copy threads);
+//   buffer_pool  netflow_amd::BufferPool::update_checksums_batch over the frames in 2176-byte slots of
+//                one pinned arena (netflow_amd::Packet, the mirror of the reference's classes);
 //   reference_1_thread / reference_threads  the reference's per-packet Packet::update_checksums() over
 //                the burst's PacketBuffers, on one thread (the switch's own loop, switch.hpp:213-294) and
 //                on `threads` threads (a SpinPool).
@@ -853,25 +855,39 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
         ptrs[i] = rp[i].get();
     }
     auto frame = [&](size_t i) -> const uint8_t* { return pristine.data() + (size_t)desc[i].off16 * 16; };
-    // arena kinds: 0 the reference's PacketBuffers, 1 the pinned ring, 2 the pageable ring
+    // netflow_amd::BufferPool slots of one pinned arena (2176-byte slots: the frames fill 69% of them)
+    netflow_amd::BufferPool bp(n, 2176, *eng);
+    std::vector<netflow_amd::PacketBuffer*> pb(n);
+    std::vector<std::unique_ptr<netflow_amd::Packet>> pp(n);
+    std::vector<netflow_amd::Packet*> pptr(n);
+    for (size_t i = 0; i < n; ++i) {
+        pb[i] = bp.allocate_buffer(desc[i].len);
+        pb[i]->set_data_len(desc[i].len);
+        pp[i].reset(new netflow_amd::Packet(pb[i]));
+        pptr[i] = pp[i].get();
+    }
+    // arena kinds: 0 the reference's PacketBuffers, 1 the pinned ring, 2 the pageable ring, 3 the pool
     auto ring_of = [&](int kind) { return kind == 1 ? pr : pageable.data(); };
+    auto data_of = [&](int kind, size_t i) -> uint8_t* {
+        if (kind == 0) return rb[i]->get_data_start_ptr();
+        if (kind == 3) return pb[i]->get_data_start_ptr();
+        return ring_of(kind) + (size_t)desc[i].off16 * 16;
+    };
     auto restore = [&](int kind) {
         copier.run(n, [&](size_t i0, size_t i1) {
-            for (size_t i = i0; i < i1; ++i) {
-                uint8_t* d = kind ? ring_of(kind) + (size_t)desc[i].off16 * 16 : rb[i]->get_data_start_ptr();
-                std::memcpy(d, frame(i), desc[i].len);
-            }
+            for (size_t i = i0; i < i1; ++i) std::memcpy(data_of(kind, i), frame(i), desc[i].len);
         });
     };
     std::vector<uint8_t> img(bytes);
     auto digest = [&](int kind) -> std::string {
-        if (!kind)
+        const bool ring = kind == 1 || kind == 2;
+        if (!ring)
             copier.run(n, [&](size_t i0, size_t i1) {
                 for (size_t i = i0; i < i1; ++i)
-                    std::memcpy(img.data() + (size_t)desc[i].off16 * 16, rb[i]->get_data_start_ptr(), desc[i].len);
+                    std::memcpy(img.data() + (size_t)desc[i].off16 * 16, data_of(kind, i), desc[i].len);
             });
         uint64_t d = 0;
-        if (nfcs_memcpy_h2d(c, d_arena, kind ? ring_of(kind) : img.data(), bytes) ||
+        if (nfcs_memcpy_h2d(c, d_arena, ring ? ring_of(kind) : img.data(), bytes) ||
             nfcs_digest_device(c, (uint8_t*)d_arena, bytes, (nfcs_desc*)d_desc, (uint32_t)n, 0, &d, nullptr))
             return "error";
         char s[32];
@@ -935,6 +951,8 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
             return nfcs_update_host(c, pageable.data(), bytes, desc.data() + off, (uint32_t)b, nullptr, 0);
         });
     if (!rc)
+        rc = path("buffer_pool", 3, [&](size_t off, size_t b) { return bp.update_checksums_batch(pptr.data() + off, b); });
+    if (!rc)
         rc = path("reference_1_thread", 0, [&](size_t off, size_t b) {
             for (size_t i = off; i < off + b; ++i) ptrs[i]->update_checksums();
             return 0;
@@ -952,6 +970,8 @@ int burstbench_mode(const std::vector<size_t>& sizes, size_t ring, double second
     }
     rp.clear();
     rb.clear();
+    pp.clear();
+    for (auto* b : pb) bp.free_buffer(b);
     nfcs_device_free(c, d_arena);
     nfcs_device_free(c, d_desc);
     nfcs_host_free(c, h_ring);

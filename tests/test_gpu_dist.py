@@ -91,11 +91,11 @@ def test_one_gpu_line_carries_c4_shard_host_and_cpu_baseline():
     # every path's result over the whole ring the reference's
     hb = d["host_bursts"]
     assert hb["rc"] == 0 and hb["parity"]["match"] is True, {k: v for k, v in hb.items() if k != "adapter"}
-    for p in ("adapter", "pinned_ring", "pageable_ring", "reference_1_thread", "reference_threads"):
+    for p in ("adapter", "pinned_ring", "pageable_ring", "buffer_pool", "reference_1_thread", "reference_threads"):
         assert set(hb[p]["bursts"]) == {"64", "256", "1024", "4096", "16384", "65536"}, p
         assert all(v["us_per_call"] > 0 for v in hb[p]["bursts"].values()), p
     assert set(hb["crossover_vs_reference_1_thread"]) == {"adapter", "pinned_ring", "pinned_ring_zero_copy",
-                                                          "pageable_ring"}
+                                                          "pageable_ring", "buffer_pool"}
     cb = d["cpu_baseline"]
     assert cb["value"] == max(x["value"] for x in cb["runs"]) and cb["value"] > 0
     assert max(x["threads"] for x in cb["runs"]) == cb["nproc"] == len(os.sched_getaffinity(0))

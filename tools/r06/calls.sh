@@ -237,4 +237,20 @@ call_t() {
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_host_ring.py tests/test_gpu_abi_errors.py tests/test_gpu_parity.py \
     -q -x --timeout 280 --timeout-method thread > $o/pytest.log 2>&1
 }
+
+call_u() {
+  # round 6, GPU call u: BufferPool bursts spanning <= NFCS_HOST_ZERO_COPY_AUTO_BYTES go to nfcs_update_host
+  # (zero-copy, the kernel reads only the frames) instead of the gather, whatever their slots' fill: the
+  # host and adapter tests, then burstbench with the buffer_pool path against the header before
+  # (poolpre: test binary built against git 9ba4fd5's packet.hpp), alternating, two rounds
+  local o=gpurun_out/r6u; mkdir -p $o
+  timeout -k 10 600 python3 -u -m pytest tests/test_netflow_adapter.py tests/test_cpp_api.py tests/test_gpu_host_ring.py \
+    -q -x --timeout 280 --timeout-method thread > $o/pytest.log 2>&1 || return 1
+  local r lib exe
+  for r in 1 2; do for lib in cur poolpre; do
+    exe=tests/cpp/_ref/netflow_adapter_test_$lib; [ $lib = cur ] && exe=tests/cpp/_ref/netflow_adapter_test
+    timeout -k 10 300 $exe burstbench 64,256,1024,4096,16384,65536 1048576 0.3 16 81cc3905092d7f44 \
+      > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
+  done; done
+}
 "call_$1"
