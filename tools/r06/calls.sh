@@ -253,4 +253,11 @@ call_u() {
       > $o/burst_${lib}_$r.json 2> $o/burst_${lib}_$r.err || return 1
   done; done
 }
+
+call_v() {
+  # round 6, GPU call v: the forward's deferred long-frame read pass without row_stage's sched_barrier
+  # (nosb; measurement build) against the product: forward C1 and 4M, three alternating rounds
+  local o=gpurun_out/r6v; mkdir -p $o
+  ab_lines $o 3 "cur nosb" "fwdc1 --op l3fwd --steps 40" "fwd4m --op l3fwd --packets 4194304 --steps 20"
+}
 "call_$1"
