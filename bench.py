@@ -747,6 +747,10 @@ def main():
         out["per_gpu_digest"] = [f"{x:016x}" for x in D.gather_u64(int(hexd, 16) if hexd else 0)]
         out["per_gpu_parity"] = [None if x < 0 else bool(x) for x in
                                  D.gather(-1.0 if parity_ok is None else float(bool(parity_ok)))]
+        if args.op == "update" and not args.no_host:
+            # every rank at once from host memory (round 6): what N GPUs, each behind its own PCIe
+            # link, take end to end — the only way the path can outrun the host's own cores (§7)
+            out["host_all_ranks"] = host_ranks_line(eng, D)
     if solo is not None:
         # the same shard on one GPU in this run (rank 0, alone), and value / (N x that)
         out["single_gpu_same_shard_GBps"] = round(solo, 2)
@@ -1063,6 +1067,48 @@ def host_line(eng, args, n, reps: int = 3):
     out["gpu_numa_node"], out["staging_numa_local"] = node, local
     out["parity"] = {"reference_digest": want, "match": ok}
     return out
+
+
+def host_ranks_line(eng, D, reps: int = 3):
+    """N > 1: C1's first 1M frames in a pinned host arena on EVERY rank (NUMA-local to its GPU through
+    the context's staging ring), nfcs_update_host on all ranks at once between barriers — the end-to-end
+    (PCIe-inclusive) rate of N GPUs each behind its own link; per call the max over ranks, best of `reps`
+    after one warm call, frames restored before each; each rank's result digest against the reference's.
+    Never `value`."""
+    n = DEFAULT_PACKETS[1]
+    d_arena, nbytes, d_desc, hdesc = eng.config_batch(1, SEED, 0, n, 128)
+    src = d_arena.download(np.uint8, nbytes)
+    frame_bytes = float(hdesc["len"].astype(np.float64).sum())
+    want = golden_digest(1, 0, n)
+    pinned = eng.host_array(nbytes)
+    mine, alls = [], []
+    try:
+        for r in range(reps + 1):
+            pinned[:] = src
+            D.barrier()
+            t0 = time.perf_counter()
+            eng.update_host(pinned, hdesc, want_status=False)
+            t = time.perf_counter() - t0
+            D.barrier()
+            if r:  # the first call warms the staging ring
+                mine.append(t)
+                alls.append(D.max(t))
+        d_arena.upload(pinned)
+        got = f"{eng.digest_device(d_arena, nbytes, d_desc, n, 0):016x}"
+    finally:
+        eng.host_free(pinned)
+        d_arena.free()
+        d_desc.free()
+    ok = want is not None and got == want
+    node, local = eng.host_numa()
+    return {"workload": f"C1: {human(n)} x 1500 B IPv4+UDP in a pinned host arena on every rank, nfcs_update_host "
+                        "on all ranks at once (frames H2D over each GPU's own link, patch records back)",
+            "timing": f"wall clock per call between barriers, the max over ranks; best of {reps}",
+            "GBps_all_ranks": round(D.sum(frame_bytes) / min(alls) / 1e9, 2),
+            "per_rank_GBps": [round(x, 2) for x in D.gather(frame_bytes / min(mine) / 1e9)],
+            "per_rank_numa_node": [int(x) for x in D.gather(float(node))],
+            "per_rank_staging_numa_local": [bool(x) for x in D.gather(float(local))],
+            "parity": {"reference_digest": want, "per_rank_match": [bool(x) for x in D.gather(float(ok))]}}
 
 
 # The other bench lines of DESIGN.md's scope table, each run as its own child bench.py (its own

@@ -48,6 +48,10 @@ def test_two_ranks_one_gpu_bench_line():
     assert d["per_gpu_frac"][0] == d["roofline"]["frac"]
     assert d["per_gpu_parity"] == [True, True]
     assert d["per_gpu_digest"][0] == d["parity"]["digest"] and len(set(d["per_gpu_digest"])) == 2
+    # and both ranks at once from host memory (each rank its own pinned C1 arena), digests the reference's
+    ha = d["host_all_ranks"]
+    assert ha["parity"]["per_rank_match"] == [True, True] and ha["GBps_all_ranks"] > 0
+    assert len(ha["per_rank_GBps"]) == 2 and all(x > 0 for x in ha["per_rank_GBps"])
     # the same shard on one GPU, timed alone in the same run, and the efficiency against it (both
     # ranks share cuda:0 here, so about 0.5)
     assert d["single_gpu_same_shard_GBps"] > 0

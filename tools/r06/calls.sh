@@ -260,4 +260,12 @@ call_v() {
   local o=gpurun_out/r6v; mkdir -p $o
   ab_lines $o 3 "cur nosb" "fwdc1 --op l3fwd --steps 40" "fwd4m --op l3fwd --packets 4194304 --steps 20"
 }
+
+call_w() {
+  # round 6, GPU call w: the N > 1 line's host_all_ranks sub-line (every rank's pinned C1 arena through
+  # nfcs_update_host at once): the 2-rank one-GPU test, a 4-rank rehearsal
+  local o=gpurun_out/r6w; mkdir -p $o
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dist.py -q -x --timeout 280 --timeout-method thread -k two_ranks > $o/pytest_dist.log 2>&1 && \
+  NFCS_BENCH_DEVICE=0 timeout -k 10 300 python3 -u bench.py --gpus 4 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus4_one_box.json 2> $o/bench_gpus4.err
+}
 "call_$1"
