@@ -268,4 +268,12 @@ call_w() {
   timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dist.py -q -x --timeout 280 --timeout-method thread -k two_ranks > $o/pytest_dist.log 2>&1 && \
   NFCS_BENCH_DEVICE=0 timeout -k 10 300 python3 -u bench.py --gpus 4 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus4_one_box.json 2> $o/bench_gpus4.err
 }
+call_x() {
+  # round 6, GPU call x: the launch-shape audit (tools/r06/shape_audit.py): 45 layouts (uniform lengths at
+  # 16- / 128-byte starts, 2048-byte ring slots, bimodal / IMIX / uniform-range mixes), auto against every
+  # shape forced by the slot hint, calls rotating over 2 batches
+  local o=gpurun_out/r6x; mkdir -p $o
+  timeout -k 10 120 python3 -u tools/r06/shape_audit.py $o/shape_audit_quick.jsonl --quick 2> $o/quick.err && \
+  timeout -k 10 600 python3 -u tools/r06/shape_audit.py $o/shape_audit.jsonl 2> $o/full.err
+}
 "call_$1"
