@@ -276,4 +276,12 @@ call_x() {
   timeout -k 10 120 python3 -u tools/r06/shape_audit.py $o/shape_audit_quick.jsonl --quick 2> $o/quick.err && \
   timeout -k 10 600 python3 -u tools/r06/shape_audit.py $o/shape_audit.jsonl 2> $o/full.err
 }
+call_y() {
+  # round 6, GPU call y: the shape audit's threshold set (tools/r06/shape_audit.py --threshold): 64 / 1500-
+  # and 64 / 1024-byte mixes by long fraction, U{64..hi}, mid-size frames in 2048 / 4096-byte ring slots
+  # against the same frames packed at the same packet count; the main set for the fused forward
+  local o=gpurun_out/r6y; mkdir -p $o
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_threshold.jsonl --threshold 2> $o/threshold.err && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_l3fwd.jsonl --l3fwd 2> $o/l3fwd.err
+}
 "call_$1"

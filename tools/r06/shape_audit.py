@@ -1,0 +1,239 @@
+"""shape_audit.py — measurement tool (not product): is the launch shape
+nfcs_update_device picks from a burst's footprint the fastest of its three for layouts OTHER than the
+configs the rule was calibrated on? Round 6 found packed C3 in the wrong shape (8-lane rows, 0.51
+against 0.64 in the short shape); this sweeps the frame-length distributions and frame alignments a
+caller may bring, device-resident, and reports per layout how far the automatic choice is from the
+best forced one.
+
+Per layout: two batches of n frames (random payload — torch.randint on the device — under IPv4 TCP/UDP
+headers of the layout's lengths, IHL 5, UDP length = frame length - 34), calls rotating over the two
+(HIP events on the stream the calls run on; the steady state of a NIC ring). Forms:
+  auto   no slot hint; each batch's footprint sample adapts the shape after its first call;
+  tiny   slot hint 256  (8-lane rows, 8 packets per one-wave workgroup, inline stores);
+  short  slot hint 1000 (16-lane rows, 7 waves/SIMD, inline stores);
+  long   slot hint 4096 (16-lane rows, line-aligned windows, deferred stores + write pass, sub-batches).
+Two alternating rounds per layout; ms per call = the lower of the two. Every form's digest of both
+batches after its calls must equal auto's (the shape picks speed only; the update is idempotent, so
+the frames after any number of calls are the frames after one). Parity against the oracle is the GPU
+tests' job (tests/test_gpu_slot_hint.py runs every shape against it).
+
+  python3 tools/r06/shape_audit.py OUT.jsonl [--quick | --threshold] [--l3fwd]
+(--l3fwd: the fused forward, nfcs_l3_forward_device, in place of the update; its shapes by the same
+hints: 8-lane rows of 6 slots / 8-lane rows of 12 slots / 16-lane rows with the deferred record pass)
+One JSON line per layout, progress on stderr."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+import netflow_amd as nf  # noqa: E402
+
+PEAK = 8.0e12
+FORMS = (("auto", 0), ("tiny", 256), ("short", 1000), ("long", 4096))
+TARGET_BYTES = 1.0e9  # arena bytes per batch (two batches: past the 256 MB memory-side cache)
+ITERS = 16
+STREAM = None
+
+
+class Ptr:
+    """A device address for the Engine calls that take a DeviceBuffer."""
+
+    def __init__(self, p):
+        self.ptr = int(p)
+
+
+def lengths(kind, n, rng):
+    if kind[0] == "uniform":  # (kind[2]: a fixed packet count for the layout)
+        return np.full(n, kind[1], dtype=np.int64)
+    if kind[0] == "range":  # U{lo..hi}
+        return rng.integers(kind[1], kind[2] + 1, n)
+    if kind[0] == "bimodal":  # 64 / 1500 (or kind[2]) with a fraction p of long frames
+        return np.where(rng.random(n) < kind[1], kind[2] if len(kind) > 2 else 1500, 64).astype(np.int64)
+    if kind[0] == "imix":  # 7:4:1 of 64 / 570 / 1500
+        return rng.permutation(np.tile(np.array([64] * 7 + [570] * 4 + [1500]), n // 12 + 1)[:n])
+    raise ValueError(kind)
+
+
+def layout(kind, align, slot, rng):
+    """(desc, arena_bytes, lens) for about TARGET_BYTES: frames packed at `align`-byte starts, or at
+    the starts of fixed `slot`-byte ring slots."""
+    probe = lengths(kind, 4096, rng)
+    per = slot if slot else float(np.mean(-(-probe // align) * align))
+    n = int(min(4 << 20, max(256 << 10, TARGET_BYTES / per))) & ~15
+    if kind[0] == "uniform" and len(kind) > 2:
+        n = kind[2]
+    lens = lengths(kind, n, rng)
+    if slot:
+        off = np.arange(n, dtype=np.int64) * slot
+    else:
+        step = -(-lens // align) * align
+        off = np.concatenate([[0], np.cumsum(step)[:-1]])
+    nbytes = int(off[-1] + (slot if slot else step[-1]))
+    desc = np.zeros(n, dtype=nf.DESC_DTYPE)
+    desc["off16"] = (off // 16).astype(np.uint32)
+    desc["len"] = lens.astype(np.uint32)
+    return desc, nbytes, lens
+
+
+def stamp(arena_t, desc, lens, seed):
+    """IPv4 TCP/UDP headers at every frame start of a random-payload device arena."""
+    dev = arena_t.device
+    off = torch.from_numpy(desc["off16"].astype(np.int64) * 16).to(dev)
+    L = torch.from_numpy(lens).to(dev)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    udp = (torch.rand(len(lens), generator=g) < 0.5).to(dev)
+    cols = {12: 0x08, 13: 0x00, 14: 0x45, 15: 0x00, 16: (L - 14) >> 8, 17: (L - 14) & 0xFF,
+            18: 0, 19: 0, 20: 0, 21: 0, 22: 64, 23: torch.where(udp, 17, 6)}
+    for c, v in cols.items():
+        v = v if torch.is_tensor(v) else torch.full_like(L, v)
+        arena_t[off + c] = v.to(torch.uint8)
+    u = off[udp]
+    arena_t[u + 38] = ((L[udp] - 34) >> 8).to(torch.uint8)
+    arena_t[u + 39] = ((L[udp] - 34) & 0xFF).to(torch.uint8)
+
+
+def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
+    rng = np.random.default_rng(seed)
+    desc, nbytes, lens = layout(kind, align, slot, rng)
+    n = len(desc)
+    batches = []
+    torch.cuda.synchronize()
+    for k in range(2):
+        a = bufs[k]
+        assert a.numel() >= nbytes
+        a[:nbytes].random_(generator=torch.Generator(device=a.device).manual_seed(seed * 2 + k))
+        stamp(a, desc, lens, seed * 2 + k)
+        batches.append((a.data_ptr(), nbytes, eng.alloc(desc.nbytes).upload(desc)))
+    torch.cuda.synchronize()
+    frame_bytes = float(lens.sum())
+    st = STREAM  # a stream of its own (the legacy default stream's handle is 0, which the engine
+    # reads as "the context's stream"): the stamps, the calls and the events all run on it
+    if op == "l3fwd":
+        # the forward (switch.hpp:279-294) with next hop i % 9 over 8 routes (index 8: no route), as
+        # bench.py's l3fwd lines; TTL 64 re-stamped before every warm / timed / parity run, each of
+        # which forwards a batch at most 10 times
+        algo = frame_bytes + 37.0 * n
+        table = eng.alloc(96).upload(np.random.default_rng(5).integers(0, 256, 96, dtype=np.uint8))
+        nh = eng.alloc(4 * n).upload((np.arange(n) % 9).astype(np.uint32))
+        extra = [table, nh]
+        call = lambda a, b, d: eng.l3_forward_device(a, b, d, nh, n, table, 8, stream=st.cuda_stream)
+
+        def restamp():
+            for k, (a, b, d) in enumerate(batches):
+                stamp(bufs[k], desc, lens, seed * 2 + k)
+    else:
+        algo = frame_bytes + 12.0 * n
+        extra = []
+        call = lambda a, b, d: eng.update_device(a, b, d, n, stream=st.cuda_stream)
+        restamp = lambda: None
+    ms = {f: [] for f, _ in FORMS}
+    digests = {}
+    auto_fp = None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rnd in range(2):
+        for form, hint in FORMS:
+            eng.set_slot_bytes(hint)
+            restamp()
+            for _ in range(2):  # warm: each batch twice (auto: its sample lands and is used)
+                for a, b, d in batches:
+                    call(a, b, d)
+            st.synchronize()
+            if form == "auto":
+                auto_fp = [eng.launch_footprint(b, d, n) for a, b, d in batches]
+            restamp()
+            e0.record(st)
+            for i in range(ITERS):  # calls rotating over the two batches, HIP events on their stream
+                call(*batches[i % 2])
+            e1.record(st)
+            e1.synchronize()
+            ms[form].append(round(e0.elapsed_time(e1) / ITERS, 4))
+            restamp()
+            if op == "l3fwd":
+                for a, b, d in batches:
+                    call(a, b, d)
+            st.synchronize()
+            dg = tuple(eng.digest_device(Ptr(a), b, d, n, stream=st.cuda_stream) for a, b, d in batches)
+            digests.setdefault(form, dg)
+            assert digests[form] == dg, (name, form)
+    eng.set_slot_bytes(0)
+    for _, _, d in batches:
+        d.free()
+    for x in extra:
+        x.free()
+    best = {f: min(v) for f, v in ms.items()}
+    fastest = min(("tiny", "short", "long"), key=lambda f: best[f])
+    shape = lambda fp: "tiny" if fp < 800 else ("short" if fp < 1200 else "long")
+    return {
+        "op": op, "layout": name, "align": align, "slot": slot, "n": n, "mean_len": round(frame_bytes / n, 1),
+        "arena_bytes_per_packet": round(nbytes / n, 1), "auto_footprint": auto_fp,
+        "auto_shape": [shape(fp) for fp in auto_fp], "ms_per_call": ms, "fastest": fastest,
+        "auto_vs_fastest": round(best["auto"] / best[fastest], 4),
+        "frac": {f: round(algo / (best[f] * 1e-3) / PEAK, 4) for f in best},
+        "digests_equal": len(set(digests.values())) == 1,
+        "digest": "%016x" % digests["auto"][0],
+    }
+
+
+def main():
+    out = sys.argv[1]
+    quick = "--quick" in sys.argv
+    op = "l3fwd" if "--l3fwd" in sys.argv else "update"
+    specs = []
+    for L in (64, 128, 256, 384, 512, 640, 704, 768, 832, 896, 1024, 1152, 1280, 1500):
+        for align in ((16,) if quick else (16, 128)):
+            specs.append((f"uniform{L}", ("uniform", L), align, 0))
+    for L in (64, 256, 512, 1024, 1500):
+        specs.append((f"ring2048_{L}", ("uniform", L), 16, 2048))
+    for p in (0.1, 0.25, 0.5, 0.75):
+        for align in (16, 128):
+            specs.append((f"bimodal{int(p * 100)}", ("bimodal", p), align, 0))
+    for align in (16, 128):
+        specs.append(("imix", ("imix",), align, 0))
+        specs.append(("U64_1500", ("range", 64, 1500), align, 0))
+        specs.append(("U64_512", ("range", 64, 512), align, 0))
+        specs.append(("U512_1500", ("range", 512, 1500), align, 0))
+        specs.append(("U64_9000", ("range", 64, 9000), align, 0))
+    if quick:
+        specs = specs[:6]
+    if "--threshold" in sys.argv:
+        # round 6, call y: where 8-lane rows stop paying for mixes of short and long frames (the
+        # fraction p of frames past one 8-lane row pass, kTinyLongMax), and mid-size frames in sparse
+        # ring slots against the same frames packed at the same n
+        specs = []
+        for p in (0.2, 0.3, 0.35, 0.4, 0.45):
+            for align in (16, 128):
+                specs.append((f"bimodal{int(p * 100)}", ("bimodal", p), align, 0))
+        for p in (0.25, 0.4, 0.6):
+            specs.append((f"bimodal1024_{int(p * 100)}", ("bimodal", p, 1024), 16, 0))
+        for hi in (1000, 1100, 1200, 1300, 1400):
+            specs.append((f"U64_{hi}", ("range", 64, hi), 16, 0))
+        for L in (640, 768, 832, 896, 960, 1024, 1088, 1152, 1216):
+            specs.append((f"ring2048_{L}", ("uniform", L), 16, 2048))
+        for L in (896, 1024, 1152):
+            specs.append((f"ring4096_{L}", ("uniform", L), 16, 4096))
+            specs.append((f"packed488K_{L}", ("uniform", L, 488272), 16, 0))
+    eng = nf.Engine(0)
+    cap = int(TARGET_BYTES * 1.3) + (64 << 20)
+    bufs = [torch.empty(cap, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    global STREAM
+    STREAM = torch.cuda.Stream()
+    assert STREAM.cuda_stream != 0
+    torch.cuda.set_stream(STREAM)
+    t0 = time.time()
+    with open(out, "w") as f:
+        for i, (name, kind, align, slot) in enumerate(specs):
+            r = audit(eng, name, kind, align, slot, 1000 + i, bufs, op)
+            f.write(json.dumps(r) + "\n")
+            f.flush()
+            print(f"[{time.time() - t0:6.1f}s] {name:14s} align {align:3d} slot {slot:4d}: auto {r['auto_shape']} "
+                  f"{min(r['ms_per_call']['auto']):.4f} ms, fastest {r['fastest']} x{r['auto_vs_fastest']}",
+                  file=sys.stderr, flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
