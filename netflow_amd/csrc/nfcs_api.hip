@@ -739,8 +739,10 @@ Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_des
     const nfcs::ObsReq req = {c->obs_dev + k, ((uint64_t)gen << 32) | n};
     if ((uint32_t)(o >> 32) != gen || !((uint32_t)o & nfcs::kObsPresent)) return {est, req};
     uint64_t mean = std::min<uint64_t>((uint32_t)o & nfcs::kObsMeanMask, est);
-    // 8-lane rows only for frames that mostly fit their one row pass (nfcs_internal.h kTinyLongMax)
-    if (mean < nfcs::kTinyMeanBytes && (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
+    // 8-lane rows only for frames that mostly fit their one row pass, or short enough on average that
+    // the packet rate bounds them (nfcs_internal.h kTinyLongMax, kTinyMixMeanBytes)
+    if (mean < nfcs::kTinyMeanBytes && mean >= nfcs::kTinyMixMeanBytes &&
+        (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
         mean = nfcs::kTinyMeanBytes;
     return {mean, req};
 }

@@ -78,9 +78,15 @@ constexpr uint64_t kTinyMeanBytes = 800;
 // 16-lane short shape (profiles/r06_c3_packed_shapes.jsonl). A wave of 8 frames of which a fraction
 // p is long continues with probability 1 - (1 - p)^8; with a continued 8-lane wave costing about
 // 1.2x two 16-lane waves (the packed C3 figures) and an uncontinued one 0.6x, they break even near
-// p = 1/8 (32 of 256): IMIX 7:4:1 (64/570/1500 B, p = 1/12) stays on 8-lane rows.
+// p = 1/8 (32 of 256): IMIX 7:4:1 (64/570/1500 B, p = 1/12) stays on 8-lane rows. The model holds
+// only where the short frames are not packet-rate bound themselves: the round-6 shape audit
+// (tools/r06/shape_audit.py, profiles/r06_y_shape_audit_threshold.jsonl) found 64-byte frames mixed
+// with 20-40% of 1024- or 1500-byte ones 4-27% faster in 8-lane rows, U{64..1000} and 64/1500 mixes
+// from 35% long frames 1-16% faster in 16-lane rows; the mean footprint splits them: below
+// kTinyMixMeanBytes a mix stays on 8-lane rows whatever its long frames.
 constexpr uint32_t kTinyRowBytes = 768;
 constexpr uint32_t kTinyLongMax = 32;
+constexpr uint64_t kTinyMixMeanBytes = 512;
 // The footprint sample's 32-bit word (sample_footprint; the burst's generation in the other 32 bits).
 constexpr uint32_t kObsPresent = 0x80000000u;
 constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)

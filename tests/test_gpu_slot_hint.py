@@ -254,20 +254,25 @@ def packed_udp(lengths, seed):
     return oracle.pack_frames(frames, align=16)
 
 
-@pytest.mark.parametrize("mix", ["c3", "imix"])
+@pytest.mark.parametrize("mix", ["c3", "imix", "bimodal25"])
 def test_packed_mix_shape_follows_its_sample(engine, mix):
     """A densely packed burst whose arena_bytes / n says 8-lane rows (< kTinyMeanBytes): the first call
     runs them and samples its frames. C3's mix (U{64..1500}, 782 B per packet packed; half its frames
     need a second 8-lane row pass) then runs the 16-lane short shape (footprint read back >= 800:
     round 6, packed C3 0.655 against 0.79-0.82 ms per call in 8-lane rows); IMIX 7:4:1 (64/570/1500 B,
-    one frame in 12 longer than a row pass) stays on 8-lane rows. Bytes and statuses equal the
-    oracle's at every call (the shape picks speed only)."""
+    one frame in 12 longer than a row pass) stays on 8-lane rows, and so does a mix of 64-byte frames
+    with 25% 1500-byte ones (many long frames, but a 424-byte mean: below kTinyMixMeanBytes, where the
+    shape audit measured 8-lane rows 15-25% faster). Bytes and statuses equal the oracle's at every
+    call (the shape picks speed only)."""
     n = 1 << 17
     if mix == "c3":
         arena, desc = oracle.gen_config(3, 20250620, 0, n)
-    else:
+    elif mix == "imix":
         lens = np.random.default_rng(62).permutation(np.tile([64] * 7 + [570] * 4 + [1500], n // 12 + 1)[:n])
         arena, desc = packed_udp(lens, 61)
+    else:
+        lens = np.random.default_rng(64).permutation(np.tile([64] * 3 + [1500], n // 4))
+        arena, desc = packed_udp(lens, 63)
     est = arena.nbytes // n
     assert est < 800, est
     ref = arena.copy()

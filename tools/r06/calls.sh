@@ -284,4 +284,18 @@ call_y() {
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_threshold.jsonl --threshold 2> $o/threshold.err && \
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_l3fwd.jsonl --l3fwd 2> $o/l3fwd.err
 }
+call_z() {
+  # round 6, GPU call z: the shape audit found the fused forward faster in 8-lane rows of 6 slots (slot hint
+  # 256) than in its long shape on 1280-1500-byte frames (call y); the bench's own forward lines (C1 1M,
+  # 4M) and the update's C1 by slot hint (0 = the product's choice, 256, 1000), three alternating rounds;
+  # then kTinyMixMeanBytes (mixes below a 512-byte mean stay on 8-lane rows): the slot-hint tests, the
+  # audit's threshold set again
+  local o=gpurun_out/r6z; mkdir -p $o
+  ab_lines $o 3 "cur" "fwd_auto --op l3fwd --steps 40" "fwd_tiny --op l3fwd --steps 40 --slot-bytes 256" \
+    "fwd_short --op l3fwd --steps 40 --slot-bytes 1000" \
+    "fwd4m_auto --op l3fwd --packets 4194304 --steps 20" "fwd4m_tiny --op l3fwd --packets 4194304 --steps 20 --slot-bytes 256" \
+    "upd_auto --steps 40" "upd_tiny --steps 40 --slot-bytes 256" && \
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_slot_hint.py -q -x --timeout 120 --timeout-method thread > $o/pytest_slot_hint.log 2>&1 && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_threshold_mix512.jsonl --threshold 2> $o/threshold.err
+}
 "call_$1"
