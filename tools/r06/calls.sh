@@ -298,4 +298,67 @@ call_z() {
   timeout -k 10 300 python3 -u -m pytest tests/test_gpu_slot_hint.py -q -x --timeout 120 --timeout-method thread > $o/pytest_slot_hint.log 2>&1 && \
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/shape_audit_threshold_mix512.jsonl --threshold 2> $o/threshold.err
 }
+call_aa() {
+  # round 6, GPU call aa: the forward's shapes on long frames by TCP share (shape_audit.py --fwdcheck
+  # --l3fwd, TTL re-stamped before the warm-up instead of right before the timed calls), then the same
+  # layouts for the update
+  local o=gpurun_out/r6aa; mkdir -p $o
+  for t in 0 0.5 1; do
+    timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdcheck_l3fwd_tcp$t.jsonl --fwdcheck --l3fwd --tcp $t 2>> $o/fwdcheck.err || return 1
+  done
+  for t in 0 1; do
+    timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdcheck_update_tcp$t.jsonl --fwdcheck --tcp $t 2>> $o/fwdcheck.err || return 1
+  done
+}
+call_ab() {
+  # round 6, GPU call ab: the forward check again with C1's and C3's own generated frames beside the audit's
+  # random-payload ones (the audit timed the forward's long shape 12% slower than bench.py does)
+  local o=gpurun_out/r6ab; mkdir -p $o
+  timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdcheck_l3fwd_gen.jsonl --fwdcheck --l3fwd --tcp 0 2> $o/fwdcheck.err && \
+  timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdcheck_update_gen.jsonl --fwdcheck --tcp 0 2>> $o/fwdcheck.err
+}
+call_ac() {
+  # round 6, GPU call ac: C1's own frames with some of the audit's header bytes on top (IP ID / flags zero,
+  # DF set, the whole stamp), forward and update, all shapes
+  local o=gpurun_out/r6ac; mkdir -p $o
+  timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdbytes_l3fwd.jsonl --fwdbytes --l3fwd --tcp 0 2> $o/fwdbytes.err && \
+  timeout -k 10 200 python3 -u tools/r06/shape_audit.py $o/fwdbytes_update.jsonl --fwdbytes --tcp 0 2>> $o/fwdbytes.err
+}
+call_ad() {
+  # round 6, GPU call ad: the forward's long shape 13-22% slower after header stamps that rewrite bytes with
+  # the values they hold (call ac, equal digests): rocprofv3 kernel stats of C1's own frames against the
+  # TTL-stamped ones, one process each — kernel time or idle time between the calls?
+  local o=gpurun_out/r6ad; mkdir -p $o
+  for l in C1_generated C1_stamp_ttl; do
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof_$l -o p -- \
+      python3 -u tools/r06/shape_audit.py $o/fwd_$l.jsonl --fwdbytes --l3fwd --tcp 0 --only $l > $o/prof_$l.log 2>&1 || return 1
+  done
+}
+call_ae() {
+  # round 6, GPU call ae: order or stamp? The same layouts in the reverse order in one process
+  # (stamped first), then alternating
+  local o=gpurun_out/r6ae; mkdir -p $o
+  timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/fwd_order.jsonl --fwdbytes --l3fwd --tcp 0 \
+    --only C1_stamp_ttl,C1_generated,C1_stamp_ttl,C1_generated,uniform1500_1M,C1_generated 2> $o/fwd_order.err
+}
+call_af() {
+  # round 6, GPU call af: stamped frames stay slow for the forward's long shape in any order (call ae);
+  # the TTL stamp followed by a whole-line rewrite of the arena (copy out and back)
+  local o=gpurun_out/r6af; mkdir -p $o
+  timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/fwd_rw.jsonl --fwdbytes --l3fwd --tcp 0 \
+    --only C1_generated,C1_stamp_ttl,C1_stamp_ttl_rw,C1_generated,C1_stamp_ttl_rw 2> $o/fwd_rw.err
+}
+call_ag() {
+  # round 6, GPU call ag: frames built on the host and uploaded whole (--host-gen) against C1's own generated
+  # frames, forward: do DMA-written frames behave like the generator's?
+  local o=gpurun_out/r6ag; mkdir -p $o
+  timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/fwd_hostgen.jsonl --fwdbytes --l3fwd --tcp 0 --host-gen \
+    --only C1_generated,uniform1500_1M,C1_generated,uniform1500_1M 2> $o/fwd_hostgen.err
+}
+call_ah() {
+  # round 6, GPU call ah: one set of buffers, the frames reset by the generator alone / + a torch TTL stamp /
+  # + a torch whole-arena copy, forward long shape and 8-lane rows (tools/r06/fwd_state.py)
+  local o=gpurun_out/r6ah; mkdir -p $o
+  timeout -k 10 300 python3 -u tools/r06/fwd_state.py > $o/fwd_state.jsonl 2> $o/fwd_state.err
+}
 "call_$1"

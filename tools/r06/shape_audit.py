@@ -17,7 +17,7 @@ batches after its calls must equal auto's (the shape picks speed only; the updat
 the frames after any number of calls are the frames after one). Parity against the oracle is the GPU
 tests' job (tests/test_gpu_slot_hint.py runs every shape against it).
 
-  python3 tools/r06/shape_audit.py OUT.jsonl [--quick | --threshold] [--l3fwd]
+  python3 tools/r06/shape_audit.py OUT.jsonl [--quick | --threshold | --fwdcheck] [--l3fwd] [--tcp F]
 (--l3fwd: the fused forward, nfcs_l3_forward_device, in place of the update; its shapes by the same
 hints: 8-lane rows of 6 slots / 8-lane rows of 12 slots / 16-lane rows with the deferred record pass)
 One JSON line per layout, progress on stderr."""
@@ -37,6 +37,11 @@ FORMS = (("auto", 0), ("tiny", 256), ("short", 1000), ("long", 4096))
 TARGET_BYTES = 1.0e9  # arena bytes per batch (two batches: past the 256 MB memory-side cache)
 ITERS = 16
 STREAM = None
+SEED_GEN = 20250620
+HOST_GEN = False  # --host-gen: frames built on the host and uploaded (the forward's long shape ran 8-17%
+# slower on frames whose headers a device kernel had stamped byte by byte, even with the same bytes:
+# calls ac-af)
+TCP_FRAC = 0.5  # --tcp F: the fraction of TCP frames (the rest UDP)
 
 
 class Ptr:
@@ -79,35 +84,93 @@ def layout(kind, align, slot, rng):
     return desc, nbytes, lens
 
 
-def stamp(arena_t, desc, lens, seed):
+def stamp(arena_t, desc, lens, seed, only=None):
     """IPv4 TCP/UDP headers at every frame start of a random-payload device arena."""
     dev = arena_t.device
     off = torch.from_numpy(desc["off16"].astype(np.int64) * 16).to(dev)
     L = torch.from_numpy(lens).to(dev)
     g = torch.Generator(device="cpu").manual_seed(seed)
-    udp = (torch.rand(len(lens), generator=g) < 0.5).to(dev)
+    udp = (torch.rand(len(lens), generator=g) >= TCP_FRAC).to(dev)
     cols = {12: 0x08, 13: 0x00, 14: 0x45, 15: 0x00, 16: (L - 14) >> 8, 17: (L - 14) & 0xFF,
             18: 0, 19: 0, 20: 0, 21: 0, 22: 64, 23: torch.where(udp, 17, 6)}
     for c, v in cols.items():
+        if only is not None and c not in only:
+            continue
         v = v if torch.is_tensor(v) else torch.full_like(L, v)
         arena_t[off + c] = v.to(torch.uint8)
+    if only is not None and 38 not in only:
+        return
     u = off[udp]
     arena_t[u + 38] = ((L[udp] - 34) >> 8).to(torch.uint8)
     arena_t[u + 39] = ((L[udp] - 34) & 0xFF).to(torch.uint8)
 
 
+def stamp_host(arena, desc, lens, seed):
+    """stamp() on a host arena (numpy): the same header bytes."""
+    off = desc["off16"].astype(np.int64) * 16
+    L = lens.astype(np.int64)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    udp = (torch.rand(len(lens), generator=g) >= TCP_FRAC).numpy()
+    cols = {12: 0x08, 13: 0x00, 14: 0x45, 15: 0x00, 16: (L - 14) >> 8, 17: (L - 14) & 0xFF,
+            18: 0, 19: 0, 20: 0, 21: 0, 22: 64, 23: np.where(udp, 17, 6)}
+    for c, v in cols.items():
+        arena[off + c] = np.asarray(v).astype(np.uint8)
+    u = off[udp]
+    arena[u + 38] = ((L[udp] - 34) >> 8).astype(np.uint8)
+    arena[u + 39] = ((L[udp] - 34) & 0xFF).astype(np.uint8)
+
+
 def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     rng = np.random.default_rng(seed)
-    desc, nbytes, lens = layout(kind, align, slot, rng)
+    gen = kind[0] == "config"  # a BASELINE config's own frames (nfcs_gen_config_device), as bench.py's
+    if gen:
+        desc, nbytes = nf.layout_config(kind[1], SEED_GEN, 0, kind[2], align)
+        lens = desc["len"].astype(np.int64)
+    else:
+        desc, nbytes, lens = layout(kind, align, slot, rng)
     n = len(desc)
     batches = []
     torch.cuda.synchronize()
+
+    host = []
+    if HOST_GEN and not gen:  # each batch built on the host and uploaded whole (DMA, full lines)
+        for k in range(2):
+            h = np.frombuffer(np.random.default_rng(seed * 2 + k).bytes(nbytes), dtype=np.uint8).copy()
+            stamp_host(h, desc, lens, seed * 2 + k)
+            host.append(torch.from_numpy(h).pin_memory())
+
+    def generate(k):
+        a, b, d = batches[k]
+        if host:
+            bufs[k][:nbytes].copy_(host[k], non_blocking=True)
+        elif gen:
+            eng.gen_config_device(kind[1], SEED_GEN + k, 0, n, Ptr(a), b, d, stream=STREAM.cuda_stream)
+            if len(kind) > 3:  # ("config", c, n, variant): some of the audit's header bytes on top
+                off = torch.from_numpy(desc["off16"].astype(np.int64) * 16).to(bufs[k].device)
+                if kind[3] in ("id0", "stamp"):
+                    for c in (18, 19, 20, 21):
+                        bufs[k][off + c] = 0
+                if kind[3] == "df":
+                    bufs[k][off + 20] = 0x40
+                    bufs[k][off + 21] = 0
+                if kind[3] == "stamp":
+                    stamp(bufs[k], desc, lens, seed * 2 + k)
+                parts = {"eth": (12, 13, 14, 15, 16, 17), "ttl": (22, 23), "udplen": (38, 39)}
+                if kind[3] in parts:
+                    stamp(bufs[k], desc, lens, seed * 2 + k, only=parts[kind[3]])
+                if kind[3] == "ttl_rw":  # the TTL stamp, then every line rewritten whole (a copy out and back)
+                    stamp(bufs[k], desc, lens, seed * 2 + k, only=(22, 23))
+                    tmp = bufs[k][:nbytes].clone()
+                    bufs[k][:nbytes].copy_(tmp)
+                    del tmp
+        else:
+            stamp(bufs[k], desc, lens, seed * 2 + k)
     for k in range(2):
         a = bufs[k]
         assert a.numel() >= nbytes
         a[:nbytes].random_(generator=torch.Generator(device=a.device).manual_seed(seed * 2 + k))
-        stamp(a, desc, lens, seed * 2 + k)
         batches.append((a.data_ptr(), nbytes, eng.alloc(desc.nbytes).upload(desc)))
+        generate(k)
     torch.cuda.synchronize()
     frame_bytes = float(lens.sum())
     st = STREAM  # a stream of its own (the legacy default stream's handle is 0, which the engine
@@ -123,8 +186,8 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
         call = lambda a, b, d: eng.l3_forward_device(a, b, d, nh, n, table, 8, stream=st.cuda_stream)
 
         def restamp():
-            for k, (a, b, d) in enumerate(batches):
-                stamp(bufs[k], desc, lens, seed * 2 + k)
+            for k in range(2):
+                generate(k)
     else:
         algo = frame_bytes + 12.0 * n
         extra = []
@@ -137,14 +200,13 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     for rnd in range(2):
         for form, hint in FORMS:
             eng.set_slot_bytes(hint)
-            restamp()
+            restamp()  # the forward: TTL 64, then 2 warm + ITERS / 2 timed forwards per batch
             for _ in range(2):  # warm: each batch twice (auto: its sample lands and is used)
                 for a, b, d in batches:
                     call(a, b, d)
             st.synchronize()
             if form == "auto":
                 auto_fp = [eng.launch_footprint(b, d, n) for a, b, d in batches]
-            restamp()
             e0.record(st)
             for i in range(ITERS):  # calls rotating over the two batches, HIP events on their stream
                 call(*batches[i % 2])
@@ -159,7 +221,18 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
             dg = tuple(eng.digest_device(Ptr(a), b, d, n, stream=st.cuda_stream) for a, b, d in batches)
             digests.setdefault(form, dg)
             assert digests[form] == dg, (name, form)
+    # the statuses of one call on batch 0 (fresh frames), by value
     eng.set_slot_bytes(0)
+    restamp()
+    d_st = eng.alloc(n)
+    a, b, d = batches[0]
+    if op == "l3fwd":
+        eng.l3_forward_device(a, b, d, nh, n, table, 8, d_st, stream=st.cuda_stream)
+    else:
+        eng.update_device(a, b, d, n, d_st, stream=st.cuda_stream)
+    st.synchronize()
+    hist = np.bincount(d_st.download(np.uint8, n), minlength=256)
+    d_st.free()
     for _, _, d in batches:
         d.free()
     for x in extra:
@@ -168,13 +241,14 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     fastest = min(("tiny", "short", "long"), key=lambda f: best[f])
     shape = lambda fp: "tiny" if fp < 800 else ("short" if fp < 1200 else "long")
     return {
-        "op": op, "layout": name, "align": align, "slot": slot, "n": n, "mean_len": round(frame_bytes / n, 1),
+        "op": op, "tcp_frac": TCP_FRAC, "layout": name, "align": align, "slot": slot, "n": n, "mean_len": round(frame_bytes / n, 1),
         "arena_bytes_per_packet": round(nbytes / n, 1), "auto_footprint": auto_fp,
         "auto_shape": [shape(fp) for fp in auto_fp], "ms_per_call": ms, "fastest": fastest,
         "auto_vs_fastest": round(best["auto"] / best[fastest], 4),
         "frac": {f: round(algo / (best[f] * 1e-3) / PEAK, 4) for f in best},
         "digests_equal": len(set(digests.values())) == 1,
         "digest": "%016x" % digests["auto"][0],
+        "status_hist": {"0x%02x" % v: int(c) for v, c in enumerate(hist) if c},
     }
 
 
@@ -199,6 +273,28 @@ def main():
         specs.append(("U64_9000", ("range", 64, 9000), align, 0))
     if quick:
         specs = specs[:6]
+    global TCP_FRAC, HOST_GEN
+    HOST_GEN = "--host-gen" in sys.argv
+    if "--tcp" in sys.argv:
+        TCP_FRAC = float(sys.argv[sys.argv.index("--tcp") + 1])
+    if "--fwdbytes" in sys.argv:
+        # round 6, call ac: which header bytes make the forward's long shape slower on the audit's
+        # frames than on C1's own (call ab: 0.309 against 0.265 ms per 1M call)
+        specs = [("C1_generated", ("config", 1, 1 << 20), 128, 0),
+                 ("C1_ipid0", ("config", 1, 1 << 20, "id0"), 128, 0),
+                 ("C1_df", ("config", 1, 1 << 20, "df"), 128, 0),
+                 ("C1_stamped", ("config", 1, 1 << 20, "stamp"), 128, 0),
+                 ("C1_stamp_eth", ("config", 1, 1 << 20, "eth"), 128, 0),
+                 ("C1_stamp_ttl", ("config", 1, 1 << 20, "ttl"), 128, 0),
+                 ("C1_stamp_udplen", ("config", 1, 1 << 20, "udplen"), 128, 0),
+                 ("C1_stamp_ttl_rw", ("config", 1, 1 << 20, "ttl_rw"), 128, 0),
+                 ("uniform1500_1M", ("uniform", 1500, 1 << 20), 128, 0)]
+    if "--fwdcheck" in sys.argv:
+        # round 6, call aa: the forward's long shape against 8-lane rows on long frames, by TCP share
+        specs = [("C1_generated", ("config", 1, 1 << 20), 128, 0), ("C3_generated_1M", ("config", 3, 1 << 20), 128, 0),
+                 ("uniform1500", ("uniform", 1500), 128, 0), ("uniform1500_1M", ("uniform", 1500, 1 << 20), 128, 0),
+                 ("uniform1280", ("uniform", 1280), 128, 0), ("ring2048_1500", ("uniform", 1500), 16, 2048),
+                 ("U64_1500", ("range", 64, 1500), 128, 0), ("bimodal50", ("bimodal", 0.5), 16, 0)]
     if "--threshold" in sys.argv:
         # round 6, call y: where 8-lane rows stop paying for mixes of short and long frames (the
         # fraction p of frames past one 8-lane row pass, kTinyLongMax), and mid-size frames in sparse
@@ -216,8 +312,11 @@ def main():
         for L in (896, 1024, 1152):
             specs.append((f"ring4096_{L}", ("uniform", L), 16, 4096))
             specs.append((f"packed488K_{L}", ("uniform", L, 488272), 16, 0))
+    if "--only" in sys.argv:
+        keep = sys.argv[sys.argv.index("--only") + 1].split(",")  # in this order, repeats allowed
+        specs = [next(x for x in specs if x[0] == k) for k in keep]
     eng = nf.Engine(0)
-    cap = int(TARGET_BYTES * 1.3) + (64 << 20)
+    cap = int(TARGET_BYTES * 1.7) + (64 << 20)  # up to 1M x 1536 B (uniform1500_1M)
     bufs = [torch.empty(cap, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
     global STREAM
     STREAM = torch.cuda.Stream()
