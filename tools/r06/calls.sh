@@ -361,4 +361,11 @@ call_ah() {
   local o=gpurun_out/r6ah; mkdir -p $o
   timeout -k 10 300 python3 -u tools/r06/fwd_state.py > $o/fwd_state.jsonl 2> $o/fwd_state.err
 }
+call_ai() {
+  # round 6, GPU call ai: after kTinyMixMeanBytes — the whole GPU suite, smoke(), the default bench line
+  local o=gpurun_out/r6ai; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
 "call_$1"
