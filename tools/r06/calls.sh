@@ -368,4 +368,10 @@ call_ai() {
   timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
   timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
 }
+call_aj() {
+  # round 6, GPU call aj: VLAN push/pop on the mixes kTinyMixMeanBytes moved to 8-lane rows (the rule is
+  # shared by every launch), auto against each VLAN shape by hint (shape_audit.py --vlanset --vlan)
+  local o=gpurun_out/r6aj; mkdir -p $o
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/vlan_audit.jsonl --vlanset --vlan 2> $o/vlan_audit.err
+}
 "call_$1"

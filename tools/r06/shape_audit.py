@@ -17,7 +17,8 @@ batches after its calls must equal auto's (the shape picks speed only; the updat
 the frames after any number of calls are the frames after one). Parity against the oracle is the GPU
 tests' job (tests/test_gpu_slot_hint.py runs every shape against it).
 
-  python3 tools/r06/shape_audit.py OUT.jsonl [--quick | --threshold | --fwdcheck] [--l3fwd] [--tcp F]
+  python3 tools/r06/shape_audit.py OUT.jsonl [--quick | --threshold | --fwdcheck | --vlanset] [--l3fwd | --vlan]
+      [--tcp F] [--host-gen] [--only NAME,...]
 (--l3fwd: the fused forward, nfcs_l3_forward_device, in place of the update; its shapes by the same
 hints: 8-lane rows of 6 slots / 8-lane rows of 12 slots / 16-lane rows with the deferred record pass)
 One JSON line per layout, progress on stderr."""
@@ -34,6 +35,9 @@ import netflow_amd as nf  # noqa: E402
 
 PEAK = 8.0e12
 FORMS = (("auto", 0), ("tiny", 256), ("short", 1000), ("long", 4096))
+# VLAN push/pop (nfcs_kernels.hip launch_vlan): 8-lane rows storing write-through (< kVlanWtMeanBytes),
+# 8-lane rows storing past the caches (< kTinyMeanBytes), 16-lane rows
+FORMS_VLAN = (("auto", 0), ("tiny_wt", 128), ("tiny", 512), ("rows16", 1000))
 TARGET_BYTES = 1.0e9  # arena bytes per batch (two batches: past the 256 MB memory-side cache)
 ITERS = 16
 STREAM = None
@@ -63,11 +67,11 @@ def lengths(kind, n, rng):
     raise ValueError(kind)
 
 
-def layout(kind, align, slot, rng):
+def layout(kind, align, slot, rng, room=0):
     """(desc, arena_bytes, lens) for about TARGET_BYTES: frames packed at `align`-byte starts, or at
     the starts of fixed `slot`-byte ring slots."""
     probe = lengths(kind, 4096, rng)
-    per = slot if slot else float(np.mean(-(-probe // align) * align))
+    per = slot if slot else float(np.mean(-(-(probe + room) // align) * align))
     n = int(min(4 << 20, max(256 << 10, TARGET_BYTES / per))) & ~15
     if kind[0] == "uniform" and len(kind) > 2:
         n = kind[2]
@@ -75,12 +79,15 @@ def layout(kind, align, slot, rng):
     if slot:
         off = np.arange(n, dtype=np.int64) * slot
     else:
-        step = -(-lens // align) * align
+        step = -(-(lens + room) // align) * align
         off = np.concatenate([[0], np.cumsum(step)[:-1]])
     nbytes = int(off[-1] + (slot if slot else step[-1]))
     desc = np.zeros(n, dtype=nf.DESC_DTYPE)
     desc["off16"] = (off // 16).astype(np.uint32)
     desc["len"] = lens.astype(np.uint32)
+    if room:  # VLAN: each frame's capacity from its start (its slot)
+        caps = np.full(n, slot, dtype=np.uint32) if slot else step.astype(np.uint32)
+        return desc, nbytes, lens, caps
     return desc, nbytes, lens
 
 
@@ -126,6 +133,8 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     if gen:
         desc, nbytes = nf.layout_config(kind[1], SEED_GEN, 0, kind[2], align)
         lens = desc["len"].astype(np.int64)
+    elif op == "vlan":
+        desc, nbytes, lens, caps = layout(kind, align, slot, rng, room=4)
     else:
         desc, nbytes, lens = layout(kind, align, slot, rng)
     n = len(desc)
@@ -188,17 +197,34 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
         def restamp():
             for k in range(2):
                 generate(k)
+    elif op == "vlan":
+        # Packet::push_vlan / pop_vlan + update_checksums (packet.hpp:655-720): each batch alternates
+        # push (VID 100, PCP 3) and pop, so after an even number of calls per batch its frames and
+        # lengths are back where they started; frames read and written whole
+        algo = 2.0 * frame_bytes + 16.0 * n
+        d_caps = eng.alloc(4 * n).upload(caps)
+        extra = [d_caps]
+        parity = {}
+        push = nf.vlan_push_op(100, 3)
+
+        def call(a, b, d):
+            k = parity.get(a, 0)
+            parity[a] = k + 1
+            eng.vlan_device(a, b, d, n, None, push if k % 2 == 0 else nf.VLAN_POP, d_caps, 0,
+                            stream=st.cuda_stream)
+        restamp = lambda: None
     else:
         algo = frame_bytes + 12.0 * n
         extra = []
         call = lambda a, b, d: eng.update_device(a, b, d, n, stream=st.cuda_stream)
         restamp = lambda: None
-    ms = {f: [] for f, _ in FORMS}
+    ms = {f: [] for f, _ in (FORMS_VLAN if op == "vlan" else FORMS)}
     digests = {}
     auto_fp = None
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    forms = FORMS_VLAN if op == "vlan" else FORMS
     for rnd in range(2):
-        for form, hint in FORMS:
+        for form, hint in forms:
             eng.set_slot_bytes(hint)
             restamp()  # the forward: TTL 64, then 2 warm + ITERS / 2 timed forwards per batch
             for _ in range(2):  # warm: each batch twice (auto: its sample lands and is used)
@@ -228,6 +254,10 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     a, b, d = batches[0]
     if op == "l3fwd":
         eng.l3_forward_device(a, b, d, nh, n, table, 8, d_st, stream=st.cuda_stream)
+    elif op == "vlan":
+        call(a, b, d)  # a push and its pop: the statuses of the pop
+        eng.vlan_device(a, b, d, n, None, nf.VLAN_POP, d_caps, 0, d_st, stream=st.cuda_stream)
+        parity[a] += 1
     else:
         eng.update_device(a, b, d, n, d_st, stream=st.cuda_stream)
     st.synchronize()
@@ -238,8 +268,11 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
     for x in extra:
         x.free()
     best = {f: min(v) for f, v in ms.items()}
-    fastest = min(("tiny", "short", "long"), key=lambda f: best[f])
-    shape = lambda fp: "tiny" if fp < 800 else ("short" if fp < 1200 else "long")
+    fastest = min((f for f in best if f != "auto"), key=lambda f: best[f])
+    if op == "vlan":
+        shape = lambda fp: "tiny_wt" if fp < 256 else ("tiny" if fp < 800 else "rows16")
+    else:
+        shape = lambda fp: "tiny" if fp < 800 else ("short" if fp < 1200 else "long")
     return {
         "op": op, "tcp_frac": TCP_FRAC, "layout": name, "align": align, "slot": slot, "n": n, "mean_len": round(frame_bytes / n, 1),
         "arena_bytes_per_packet": round(nbytes / n, 1), "auto_footprint": auto_fp,
@@ -255,7 +288,7 @@ def audit(eng, name, kind, align, slot, seed, bufs, op="update"):
 def main():
     out = sys.argv[1]
     quick = "--quick" in sys.argv
-    op = "l3fwd" if "--l3fwd" in sys.argv else "update"
+    op = "l3fwd" if "--l3fwd" in sys.argv else ("vlan" if "--vlan" in sys.argv else "update")
     specs = []
     for L in (64, 128, 256, 384, 512, 640, 704, 768, 832, 896, 1024, 1152, 1280, 1500):
         for align in ((16,) if quick else (16, 128)):
@@ -277,6 +310,13 @@ def main():
     HOST_GEN = "--host-gen" in sys.argv
     if "--tcp" in sys.argv:
         TCP_FRAC = float(sys.argv[sys.argv.index("--tcp") + 1])
+    if "--vlanset" in sys.argv:
+        # round 6, call aj: VLAN push/pop on the mixes kTinyMixMeanBytes moved (its launches share the rule)
+        specs = [(f"bimodal{int(p * 100)}", ("bimodal", p), 16, 0) for p in (0.1, 0.2, 0.25, 0.3, 0.35, 0.5)]
+        specs += [("bimodal1024_40", ("bimodal", 0.4, 1024), 16, 0), ("U64_1000", ("range", 64, 1000), 16, 0),
+                  ("U64_1500", ("range", 64, 1500), 16, 0), ("imix", ("imix",), 16, 0),
+                  ("uniform64", ("uniform", 64), 16, 0), ("uniform1500", ("uniform", 1500), 128, 0),
+                  ("ring2048_1024", ("uniform", 1024), 16, 2048)]
     if "--fwdbytes" in sys.argv:
         # round 6, call ac: which header bytes make the forward's long shape slower on the audit's
         # frames than on C1's own (call ab: 0.309 against 0.265 ms per 1M call)
