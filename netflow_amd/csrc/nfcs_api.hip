@@ -710,7 +710,7 @@ int update_host_zero_copy(nfcs_ctx* c, uint8_t* h_arena, uint64_t arena_bytes,
 // result), and the next call on the same burst (descriptor array, n and arena_bytes; up to kObsSlots
 // bursts tracked, least recently used replaced) launches in the shape that sample says: a NIC ring
 // reusing its descriptor arrays adapts after one call, with no hint and no host sync.
-struct Shape { uint64_t mean; nfcs::ObsReq obs; };
+struct Shape { uint64_t mean; nfcs::ObsReq obs; uint32_t bits = 0; };  // bits: the sample's kObsUnaligned / kObsMixed
 // The burst's observation slot, or -1 (no side effects).
 int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
     for (int k = 0; k < nfcs_ctx::kObsSlots; ++k) {
@@ -724,7 +724,9 @@ int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
 // Estimates that a sample can correct: "long" (a burst inside a larger ring), and "8-lane rows" (a
 // densely packed mix whose frames often need a second 8-lane row pass; round 6).
 bool sampled_estimate(uint64_t est) { return est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes; }
-Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot) {
+// mix_mean: the op's kTinyMixMeanBytes (the update and the forward) or kVlanMixMeanBytes (VLAN).
+Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot,
+                 uint64_t mix_mean = nfcs::kTinyMixMeanBytes) {
     *slot = -1;
     if (c->slot_bytes) return {c->slot_bytes, {}};
     if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
@@ -741,14 +743,15 @@ Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_des
     uint64_t mean = std::min<uint64_t>((uint32_t)o & nfcs::kObsMeanMask, est);
     // 8-lane rows only for frames that mostly fit their one row pass, or short enough on average that
     // the packet rate bounds them (nfcs_internal.h kTinyLongMax, kTinyMixMeanBytes)
-    if (mean < nfcs::kTinyMeanBytes && mean >= nfcs::kTinyMixMeanBytes &&
+    if (mean < nfcs::kTinyMeanBytes && mean >= mix_mean &&
         (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
         mean = nfcs::kTinyMeanBytes;
-    return {mean, req};
+    return {mean, req, (uint32_t)o & (nfcs::kObsUnaligned | nfcs::kObsMixed)};
 }
-Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n) {
+Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n,
+                   uint64_t mix_mean = nfcs::kTinyMixMeanBytes) {
     int k = -1;
-    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k);
+    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, mix_mean);
     if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && sampled_estimate(arena_bytes / n)) {
         // a burst not seen lately: the least recently used slot, under a new generation
         k = 0;
@@ -922,9 +925,9 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
-    const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes);
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
-                               cap_all, d_status, pick(c, stream), sh.mean, sh.obs));
+                               cap_all, d_status, pick(c, stream), sh.mean, sh.obs, sh.bits));
     return NFCS_OK;
 }
 
@@ -1498,10 +1501,10 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it) {
-        const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
+        const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes);
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
                                    (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
-                                   sh.mean, sh.obs));
+                                   sh.mean, sh.obs, sh.bits));
     }
     NFCS_HIP(hipEventRecord(c->ev1, st));
     NFCS_HIP(hipEventSynchronize(c->ev1));

@@ -91,10 +91,25 @@ constexpr uint64_t kTinyMixMeanBytes = 512;
 constexpr uint32_t kObsPresent = 0x80000000u;
 constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)
 constexpr uint32_t kObsMeanMask = 0xFFFFFu;  // bits 0-19: the mean of the lengths rounded up to 128
+// bit 29: more than kObsUnalignedMax of the sampled frames start off a 128-byte line (they share lines
+// with their neighbours); bit 30: the sampled lengths, rounded up to 128, span more than 128 bytes
+constexpr uint32_t kObsUnaligned = 1u << 29;
+constexpr uint32_t kObsMixed = 1u << 30;
+constexpr uint32_t kObsUnalignedMax = 32;
 // VLAN push/pop below this mean footprint writes its frames write-through (`sc1`), at or above it
 // past the caches (`sc0 sc1 nt`): 1M frames in 128-byte slots 177 vs 181 µs, in 384 / 640-byte
-// slots 212-216 vs 208 / 258 vs 245 µs, C1 0.698-0.704 vs 0.728-0.731.
+// slots 212-216 vs 208 / 258 vs 245 µs, C1 0.698-0.704 vs 0.728-0.731. In 8-lane
+// rows that holds only for frames of one length starting on lines: a sample that finds frames off
+// their lines or lengths that vary (kObsUnaligned / kObsMixed) writes write-through at any mean below
+// kTinyMeanBytes — round 6 shape audit (profiles/r06_ak_vlan_audit2.jsonl): packed 384-768-byte frames
+// 14-43% faster write-through, IMIX 15-31%, 64/1500 mixes 28-47%; uniform 384-640-byte frames at
+// 128-byte starts 1-21% faster past the caches.
 constexpr uint64_t kVlanWtMeanBytes = 256;
+// VLAN's kTinyMixMeanBytes: its write-through 8-lane rows keep mixes with many long frames up to a higher
+// mean than the checksum kernel's (same audit: U{64..1000} and 64/1500 with 30% long frames, 540-550 B,
+// 17-24% faster in them than in 16-lane rows; 64/1500 half and half and packed C3, 782-784 B, 16-22%
+// slower).
+constexpr uint64_t kVlanMixMeanBytes = 640;
 // Dynamic LDS per 256-thread checksum workgroup (unused): 5 workgroups = 5 waves/SIMD per CU.
 constexpr unsigned kRowsLdsPad = 30720;
 // The same for 6 workgroups = 6 waves/SIMD: the forward's deferred read pass, the stream-read forms.
@@ -143,7 +158,7 @@ hipError_t launch_l3_forward(const DevInfo& di, uint8_t* arena, uint64_t arena_b
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
                        uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes = 0,
-                       ObsReq obs = {});
+                       ObsReq obs = {}, uint32_t sample_bits = 0);
 
 hipError_t launch_flow_keys(const DevInfo& di, const uint8_t* arena, uint64_t arena_bytes,
                             const nfcs_desc* desc, uint32_t n, nfcs_flow_key* keys,

@@ -724,21 +724,33 @@ DEV void signal_done(const DoneReq& d, uint32_t nblocks) {
 // alone says 8-lane rows; nfcs_api.hip launch_shape). Speed only.
 DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint32_t lane, uint64_t* obs) {
     const uint32_t n = (uint32_t)tag;
-    uint32_t s = 0, c = 0;
+    uint32_t s = 0, c = 0, u = 0, lo = 0xFFFFFFFFu, hi = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t len = desc[(uint32_t)(((uint64_t)(4u * lane + k) * n) >> 8)].len;
-        s += ((len < 0xFFFFu ? len : 0xFFFFu) + 127u) & ~127u;
-        c += len > kTinyRowBytes ? 1u : 0u;
+        const nfcs_desc d = desc[(uint32_t)(((uint64_t)(4u * lane + k) * n) >> 8)];
+        const uint32_t r = ((d.len < 0xFFFFu ? d.len : 0xFFFFu) + 127u) & ~127u;
+        s += r;
+        c += d.len > kTinyRowBytes ? 1u : 0u;
+        u += (d.off16 & 7u) ? 1u : 0u;
+        lo = min(lo, r);
+        hi = max(hi, r);
     }
     s = row_sum<16>(s);
     c = row_sum<16>(c);
-    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)s, 0) + (uint32_t)__builtin_amdgcn_readlane((int)s, 16) +
-                       (uint32_t)__builtin_amdgcn_readlane((int)s, 32) + (uint32_t)__builtin_amdgcn_readlane((int)s, 48);
-    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)c, 0) + (uint32_t)__builtin_amdgcn_readlane((int)c, 16) +
-                       (uint32_t)__builtin_amdgcn_readlane((int)c, 32) + (uint32_t)__builtin_amdgcn_readlane((int)c, 48);
+    u = row_sum<16>(u);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {  // wave min / max of the rounded lengths (one wave, once per launch)
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, m));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, m));
+    }
+    auto wave_total = [](uint32_t v) {
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+               (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    };
+    const uint32_t t = wave_total(s), l = wave_total(c), un = wave_total(u);
+    const uint32_t bits = (un > kObsUnalignedMax ? kObsUnaligned : 0u) | (hi - lo > 128u ? kObsMixed : 0u);
     if (lane == 0)
-        __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | kObsPresent | (l << kObsLongShift) | (t >> 8),
+        __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | kObsPresent | bits | (l << kObsLongShift) | (t >> 8),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -1874,7 +1886,7 @@ __global__ __launch_bounds__(kBlock) void vlan_rows_kernel(uint8_t* __restrict__
 hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, nfcs_desc* desc,
                        uint32_t n, const uint32_t* ops, uint32_t op_all, const uint32_t* caps,
                        uint32_t cap_all, uint8_t* status, hipStream_t stream, uint64_t slot_bytes,
-                       ObsReq obs) {
+                       ObsReq obs, uint32_t sample_bits) {
     (void)di;
     if (n == 0) return hipSuccess;
     // Long frames continue in batches of 6 slots (128 VGPRs, 4 waves/SIMD); batches of 2 slots
@@ -1883,10 +1895,12 @@ hipError_t launch_vlan(const DevInfo& di, uint8_t* arena, uint64_t arena_bytes, 
     // slower here). Frame stores past the caches (`sc0 sc1 nt`, round 2 session 3): C1 push/pop
     // +4.5%, 1M 256 / 512-byte frames +2-5% against write-through `sc1` (itself +1.2% over plain
     // stores); frames in slots under 256 B keep `sc1` (64-byte frames: 177 vs 181 µs per 1M).
-    // Short frames (mean footprint < kTinyMeanBytes): 8-lane rows, 8 packets per wave (§5g).
+    // Short frames (mean footprint < kTinyMeanBytes): 8-lane rows, 8 packets per wave (§5g), their
+    // stores write-through also when the burst's sample found frames off their lines or of varying
+    // lengths (sample_bits; nfcs_internal.h kVlanWtMeanBytes).
     const uint64_t mean = shape_mean(arena_bytes, n, slot_bytes);
     const dim3 g8((n + 31u) / 32u), g16((n + 15u) / 16u);
-    if (mean < kVlanWtMeanBytes)
+    if (mean < kVlanWtMeanBytes || (mean < kTinyMeanBytes && (sample_bits & (kObsUnaligned | kObsMixed))))
         hipLaunchKernelGGL((vlan_rows_kernel<6, 6, VST_WT, 8>), g8, dim3(kBlock), 0, stream, arena, arena_bytes,
                            desc, n, ops, op_all, caps, cap_all, status, obs.slot, obs.tag);
     else if (mean < kTinyMeanBytes)

@@ -341,3 +341,39 @@ def test_packed_mix_forward_and_vlan_follow_the_sample(engine):
         engine.set_slot_bytes(0)
         for b in (d_arena, d_desc, d_nh, d_tab, d_caps, d_st):
             b.free()
+
+
+@pytest.mark.parametrize("align", [16, 128])
+def test_packed_imix_vlan_follows_the_sample(engine, align):
+    """VLAN push/pop on IMIX 7:4:1 (mean footprint under kTinyMeanBytes: 8-lane rows). The first call
+    samples the frames; from the second on, frames of varying lengths (and, packed at 16-byte starts,
+    frames sharing lines) store write-through in 8-lane rows (nfcs_internal.h kVlanWtMeanBytes; the
+    round-6 audit measured them 15-31% faster than past the caches). Each call's bytes, statuses and
+    lengths equal the oracle's applied as many times (the store policy picks speed only)."""
+    n = 1 << 16
+    lens = np.random.default_rng(65).permutation(np.tile([64] * 7 + [570] * 4 + [1500], n // 12 + 1)[:n])
+    arena0, desc0 = packed_udp(lens, 66)
+    frames = oracle.unpack_frames(arena0, desc0)
+    arena, desc = oracle.pack_frames(frames, align=align, room=4)
+    caps = np.diff(np.append(desc["off16"].astype(np.int64), arena.nbytes // 16)) * 16
+    engine.set_slot_bytes(0)
+    d_arena = engine.alloc(arena.nbytes).upload(arena)
+    d_desc = engine.alloc(desc.nbytes).upload(desc)
+    d_caps = engine.alloc(4 * n).upload(np.ascontiguousarray(caps, dtype=np.uint32))
+    d_st = engine.alloc(n)
+    try:
+        assert engine.launch_footprint(arena.nbytes, d_desc, n) < 800
+        ref, rdesc = arena.copy(), desc.copy()
+        for k, op in enumerate(["push", "pop", "push", "pop"]):
+            word = oracle.vlan_op(op, 200 + k, 5)
+            rst = oracle.vlan_batch(ref, rdesc, None, caps, op_all=word)
+            engine.vlan_device(d_arena, arena.nbytes, d_desc, n, None, word, d_caps, 0, d_st)
+            engine.sync()
+            assert np.array_equal(d_st.download(np.uint8, n), rst), op
+            assert np.array_equal(d_desc.download(np.dtype(desc.dtype), n), rdesc), op
+            assert np.array_equal(d_arena.download(np.uint8, arena.nbytes), ref), op
+        assert engine.launch_footprint(arena.nbytes, d_desc, n) < 800  # still 8-lane rows
+    finally:
+        engine.set_slot_bytes(0)
+        for b in (d_arena, d_desc, d_caps, d_st):
+            b.free()

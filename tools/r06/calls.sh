@@ -374,4 +374,29 @@ call_aj() {
   local o=gpurun_out/r6aj; mkdir -p $o
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/vlan_audit.jsonl --vlanset --vlan 2> $o/vlan_audit.err
 }
+call_ak() {
+  # round 6, GPU call ak: VLAN push/pop shapes by frame alignment: uniform 128-1024 B, IMIX, 64/1500 and
+  # U{64..hi} mixes at 16- and 128-byte starts, 2 KiB ring slots (shape_audit.py --vlanset2 --vlan)
+  local o=gpurun_out/r6ak; mkdir -p $o
+  timeout -k 10 500 python3 -u tools/r06/shape_audit.py $o/vlan_audit2.jsonl --vlanset2 --vlan 2> $o/vlan_audit2.err
+}
+call_al() {
+  # round 6, GPU call al: VLAN's 8-lane store policy from the sample's new bits (frames off their lines,
+  # varying lengths -> write-through): the slot-hint and VLAN GPU tests, the VLAN audit sets again, the
+  # VLAN C1 bench line
+  local o=gpurun_out/r6al; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_vlan.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 && \
+  timeout -k 10 500 python3 -u tools/r06/shape_audit.py $o/vlan_audit2.jsonl --vlanset2 --vlan 2> $o/vlan_audit2.err && \
+  timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/vlan_audit.jsonl --vlanset --vlan 2> $o/vlan_audit.err && \
+  timeout -k 10 200 python3 -u bench.py --op vlan --steps 40 --no-cpu --no-host --no-c4 --no-replay --no-mix --no-ops > $o/bench_vlan.json 2> $o/bench_vlan.err
+}
+call_am() {
+  # round 6, GPU call am: kVlanMixMeanBytes (VLAN keeps mixes on write-through 8-lane rows up to a 640-byte
+  # mean): the same tests, audits and VLAN C1 line as call al
+  local o=gpurun_out/r6am; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_vlan.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 && \
+  timeout -k 10 500 python3 -u tools/r06/shape_audit.py $o/vlan_audit2.jsonl --vlanset2 --vlan 2> $o/vlan_audit2.err && \
+  timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/vlan_audit.jsonl --vlanset --vlan 2> $o/vlan_audit.err && \
+  timeout -k 10 200 python3 -u bench.py --op vlan --steps 40 --no-cpu --no-host --no-c4 --no-replay --no-mix --no-ops > $o/bench_vlan.json 2> $o/bench_vlan.err
+}
 "call_$1"

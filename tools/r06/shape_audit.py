@@ -317,6 +317,18 @@ def main():
                   ("U64_1500", ("range", 64, 1500), 16, 0), ("imix", ("imix",), 16, 0),
                   ("uniform64", ("uniform", 64), 16, 0), ("uniform1500", ("uniform", 1500), 128, 0),
                   ("ring2048_1024", ("uniform", 1024), 16, 2048)]
+    if "--vlanset2" in sys.argv:
+        # round 6, call ak: VLAN's store policy by frame alignment (call aj: on mixes packed at 16-byte
+        # starts 8-lane rows storing write-through beat those storing past the caches by 15-45%)
+        specs = []
+        for align in (16, 128):
+            for L in (128, 256, 384, 512, 640, 768, 1024):
+                specs.append((f"uniform{L}", ("uniform", L), align, 0))
+            specs += [("imix", ("imix",), align, 0), ("bimodal20", ("bimodal", 0.2), align, 0),
+                      ("bimodal30", ("bimodal", 0.3), align, 0), ("bimodal50", ("bimodal", 0.5), align, 0),
+                      ("U64_1000", ("range", 64, 1000), align, 0), ("U64_1500", ("range", 64, 1500), align, 0),
+                      ("U64_512", ("range", 64, 512), align, 0)]
+        specs += [("ring2048_512", ("uniform", 512), 16, 2048), ("ring2048_256", ("uniform", 256), 16, 2048)]
     if "--fwdbytes" in sys.argv:
         # round 6, call ac: which header bytes make the forward's long shape slower on the audit's
         # frames than on C1's own (call ab: 0.309 against 0.265 ms per 1M call)
