@@ -399,4 +399,10 @@ call_am() {
   timeout -k 10 300 python3 -u tools/r06/shape_audit.py $o/vlan_audit.jsonl --vlanset --vlan 2> $o/vlan_audit.err && \
   timeout -k 10 200 python3 -u bench.py --op vlan --steps 40 --no-cpu --no-host --no-c4 --no-replay --no-mix --no-ops > $o/bench_vlan.json 2> $o/bench_vlan.err
 }
+call_an() {
+  # round 6, GPU call an: the fused forward on the threshold set (64/1500, 64/1024 mixes, U{64..hi}, ring
+  # slots) with kTinyMixMeanBytes in place: 8-lane rows against the short-mix rows on mixes
+  local o=gpurun_out/r6an; mkdir -p $o
+  timeout -k 10 500 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err
+}
 "call_$1"
