@@ -405,4 +405,14 @@ call_an() {
   local o=gpurun_out/r6an; mkdir -p $o
   timeout -k 10 500 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err
 }
+call_ao() {
+  # round 6, GPU call ao: after the VLAN store rule — the whole GPU suite, smoke(), the default bench line,
+  # and rocprofv3 kernel stats of the C1 line
+  local o=gpurun_out/r6ao; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof_c1 -o p -- \
+    python3 bench.py --steps 20 --no-cpu --no-host --no-c4 --no-replay --no-mix --no-ops > $o/prof_c1.log 2>&1
+}
 "call_$1"
