@@ -724,9 +724,10 @@ int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
 // Estimates that a sample can correct: "long" (a burst inside a larger ring), and "8-lane rows" (a
 // densely packed mix whose frames often need a second 8-lane row pass; round 6).
 bool sampled_estimate(uint64_t est) { return est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes; }
-// mix_mean: the op's kTinyMixMeanBytes (the update and the forward) or kVlanMixMeanBytes (VLAN).
+// mix_mean: the op's kTinyMixMeanBytes (the update and the forward) or kVlanMixMeanBytes (VLAN);
+// ring_rows8: mid-size frames of one length on their own lines in a ring run 8-lane rows (not VLAN).
 Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot,
-                 uint64_t mix_mean = nfcs::kTinyMixMeanBytes) {
+                 uint64_t mix_mean = nfcs::kTinyMixMeanBytes, bool ring_rows8 = true) {
     *slot = -1;
     if (c->slot_bytes) return {c->slot_bytes, {}};
     if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
@@ -746,12 +747,18 @@ Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_des
     if (mean < nfcs::kTinyMeanBytes && mean >= mix_mean &&
         (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
         mean = nfcs::kTinyMeanBytes;
-    return {mean, req, (uint32_t)o & (nfcs::kObsUnaligned | nfcs::kObsMixed)};
+    const uint32_t bits = (uint32_t)o & (nfcs::kObsUnaligned | nfcs::kObsMixed);
+    // a ring (the sample corrected a "long" estimate) of mid-size frames of one length, each on its own
+    // lines: 8-lane rows (nfcs_internal.h, after kTinyMixMeanBytes)
+    if (ring_rows8 && !bits && est >= nfcs::kSmallMeanBytes && mean >= nfcs::kTinyMeanBytes &&
+        mean < nfcs::kSmallMeanBytes)
+        mean = nfcs::kTinyMeanBytes - 1;
+    return {mean, req, bits};
 }
 Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n,
-                   uint64_t mix_mean = nfcs::kTinyMixMeanBytes) {
+                   uint64_t mix_mean = nfcs::kTinyMixMeanBytes, bool ring_rows8 = true) {
     int k = -1;
-    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, mix_mean);
+    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, mix_mean, ring_rows8);
     if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && sampled_estimate(arena_bytes / n)) {
         // a burst not seen lately: the least recently used slot, under a new generation
         k = 0;
@@ -925,7 +932,7 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
-    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes);
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes, false);
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
                                cap_all, d_status, pick(c, stream), sh.mean, sh.obs, sh.bits));
     return NFCS_OK;
@@ -1501,7 +1508,7 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it) {
-        const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes);
+        const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes, false);
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
                                    (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
                                    sh.mean, sh.obs, sh.bits));

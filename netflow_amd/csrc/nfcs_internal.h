@@ -87,6 +87,13 @@ constexpr uint64_t kTinyMeanBytes = 800;
 constexpr uint32_t kTinyRowBytes = 768;
 constexpr uint32_t kTinyLongMax = 32;
 constexpr uint64_t kTinyMixMeanBytes = 512;
+// A burst inside a larger ring whose sample finds frames of one length (rounded to 128 bytes), each
+// starting on a line, with a footprint between kTinyMeanBytes and kSmallMeanBytes runs 8-lane rows
+// rather than the short shape (nfcs_api.hip peek_shape; the update and the forward, not VLAN): round 6
+// audit, 832-1216-byte frames in 2 KiB ring slots 11-16% faster (update) and 8-13% (forward), in 4 KiB
+// slots within 3% either way (profiles/r06_y_shape_audit_threshold.jsonl, r06_an_fwd_threshold.jsonl).
+// Packed layouts of such frames are not sampled (their estimate is exact) and keep the short shape,
+// where 8-lane rows measured -5% to +11% depending on the batch.
 // The footprint sample's 32-bit word (sample_footprint; the burst's generation in the other 32 bits).
 constexpr uint32_t kObsPresent = 0x80000000u;
 constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)

@@ -415,4 +415,12 @@ call_ao() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof_c1 -o p -- \
     python3 bench.py --steps 20 --no-cpu --no-host --no-c4 --no-replay --no-mix --no-ops > $o/prof_c1.log 2>&1
 }
+call_ap() {
+  # round 6, GPU call ap: mid-size frames of one length in a ring -> 8-lane rows (peek_shape ring_rows8): the
+  # slot-hint and line-window tests, the threshold audit for the update and the forward
+  local o=gpurun_out/r6ap; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_line_windows.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/upd_threshold.jsonl --threshold 2> $o/upd_threshold.err && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err
+}
 "call_$1"
