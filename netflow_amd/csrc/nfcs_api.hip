@@ -724,10 +724,15 @@ int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
 // Estimates that a sample can correct: "long" (a burst inside a larger ring), and "8-lane rows" (a
 // densely packed mix whose frames often need a second 8-lane row pass; round 6).
 bool sampled_estimate(uint64_t est) { return est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes; }
-// mix_mean: the op's kTinyMixMeanBytes (the update and the forward) or kVlanMixMeanBytes (VLAN);
-// ring_rows8: mid-size frames of one length on their own lines in a ring run 8-lane rows (not VLAN).
+// Each op's use of the sample (nfcs_internal.h, after kTinyMixMeanBytes): the mean from which a mix with
+// many long frames leaves 8-lane rows, whether mid-size frames of one length in a ring take 8-lane rows,
+// and whether a mix with hardly any mid-length frames (64 / 1500-byte traffic) stays on them.
+struct ShapeRule { uint64_t mix_mean; bool ring_rows8; bool bimodal_rows8; };
+constexpr ShapeRule kUpdateRule = {nfcs::kTinyMixMeanBytes, true, false};
+constexpr ShapeRule kFwdRule = {nfcs::kTinyMixMeanBytes, true, true};
+constexpr ShapeRule kVlanRule = {nfcs::kVlanMixMeanBytes, false, false};
 Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot,
-                 uint64_t mix_mean = nfcs::kTinyMixMeanBytes, bool ring_rows8 = true) {
+                 const ShapeRule& rule = kUpdateRule) {
     *slot = -1;
     if (c->slot_bytes) return {c->slot_bytes, {}};
     if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
@@ -743,22 +748,24 @@ Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_des
     if ((uint32_t)(o >> 32) != gen || !((uint32_t)o & nfcs::kObsPresent)) return {est, req};
     uint64_t mean = std::min<uint64_t>((uint32_t)o & nfcs::kObsMeanMask, est);
     // 8-lane rows only for frames that mostly fit their one row pass, or short enough on average that
-    // the packet rate bounds them (nfcs_internal.h kTinyLongMax, kTinyMixMeanBytes)
-    if (mean < nfcs::kTinyMeanBytes && mean >= mix_mean &&
+    // the packet rate bounds them (nfcs_internal.h kTinyLongMax, kTinyMixMeanBytes), or — the forward —
+    // a mix of short and full-size frames with hardly any in between (kObsMidShift)
+    const bool bimodal = rule.bimodal_rows8 && (((uint32_t)o >> nfcs::kObsMidShift) & 7u) < nfcs::kObsMidMin8;
+    if (mean < nfcs::kTinyMeanBytes && mean >= rule.mix_mean && !bimodal &&
         (((uint32_t)o >> nfcs::kObsLongShift) & 0x1FFu) > nfcs::kTinyLongMax)
         mean = nfcs::kTinyMeanBytes;
     const uint32_t bits = (uint32_t)o & (nfcs::kObsUnaligned | nfcs::kObsMixed);
     // a ring (the sample corrected a "long" estimate) of mid-size frames of one length, each on its own
     // lines: 8-lane rows (nfcs_internal.h, after kTinyMixMeanBytes)
-    if (ring_rows8 && !bits && est >= nfcs::kSmallMeanBytes && mean >= nfcs::kTinyMeanBytes &&
+    if (rule.ring_rows8 && !bits && est >= nfcs::kSmallMeanBytes && mean >= nfcs::kTinyMeanBytes &&
         mean < nfcs::kSmallMeanBytes)
         mean = nfcs::kTinyMeanBytes - 1;
     return {mean, req, bits};
 }
 Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n,
-                   uint64_t mix_mean = nfcs::kTinyMixMeanBytes, bool ring_rows8 = true) {
+                   const ShapeRule& rule = kUpdateRule) {
     int k = -1;
-    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, mix_mean, ring_rows8);
+    Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, rule);
     if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && sampled_estimate(arena_bytes / n)) {
         // a burst not seen lately: the least recently used slot, under a new generation
         k = 0;
@@ -791,7 +798,7 @@ int l3_forward_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_bytes, const
                       uint8_t* d_status, hipStream_t st) {
     const bool dfr = n > nfcs::kFwdDeferAbovePackets;
     if (dfr) NFCS_HIP(acquire_ws(c, nfcs::kSubBatchPackets, st));
-    const Shape sh = launch_shape(c, arena_bytes, d_desc, n);
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, kFwdRule);
     NFCS_HIP(nfcs::launch_l3_forward(c->di, d_arena, arena_bytes, d_desc, d_nh, n, d_table, table_n,
                                      d_status, dfr ? c->ws : nullptr, st, sh.mean, sh.obs));
     if (dfr) NFCS_HIP(release_ws(c, st));
@@ -932,7 +939,7 @@ NFCS_API int nfcs_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena_byte
     if (n == 0) return NFCS_OK;
     if (!d_arena || !d_desc || ((uintptr_t)d_arena & 15u)) return NFCS_EINVAL;
     if (((uintptr_t)d_ops & 3u) || ((uintptr_t)d_caps & 3u)) return NFCS_EINVAL;
-    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes, false);
+    const Shape sh = launch_shape(c, arena_bytes, d_desc, n, kVlanRule);
     NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, d_ops, op_all, d_caps,
                                cap_all, d_status, pick(c, stream), sh.mean, sh.obs, sh.bits));
     return NFCS_OK;
@@ -1508,7 +1515,7 @@ NFCS_API int nfcs_time_vlan_device(nfcs_ctx* c, uint8_t* d_arena, uint64_t arena
     hipStream_t st = pick(c, stream);
     NFCS_HIP(hipEventRecord(c->ev0, st));
     for (int it = 0; it < iters; ++it) {
-        const Shape sh = launch_shape(c, arena_bytes, d_desc, n, nfcs::kVlanMixMeanBytes, false);
+        const Shape sh = launch_shape(c, arena_bytes, d_desc, n, kVlanRule);
         NFCS_HIP(nfcs::launch_vlan(c->di, d_arena, arena_bytes, d_desc, n, nullptr,
                                    (it & 1) ? op_alt : op_all, nullptr, cap_all, d_status, st,
                                    sh.mean, sh.obs, sh.bits));

@@ -97,7 +97,16 @@ constexpr uint64_t kTinyMixMeanBytes = 512;
 // The footprint sample's 32-bit word (sample_footprint; the burst's generation in the other 32 bits).
 constexpr uint32_t kObsPresent = 0x80000000u;
 constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)
-constexpr uint32_t kObsMeanMask = 0xFFFFFu;  // bits 0-19: the mean of the lengths rounded up to 128
+constexpr uint32_t kObsMeanMask = 0x1FFFFu;  // bits 0-16: the mean of the lengths rounded up to 128
+// bits 17-19: how many sampled frames have a rounded length above 128 and at most 1408 bytes (neither
+// minimum-size nor full-size), in 32s, at most 7; a mix with fewer than kObsMidMin8 such 32s is
+// bimodal (64 / 1500-byte traffic). The fused forward keeps such mixes on 8-lane rows of 6 slots at any
+// mean below kTinyMeanBytes: round 6 audit, 64/1500 mixes with 35-50% full-size frames packed at 16-byte
+// starts 24-34% faster there than in its 12-slot short-mix rows, at 128-byte starts within 3%; U{64..hi}
+// mixes and packed C3, whose frames fill the middle, keep the short-mix rows (1-14% faster in them;
+// profiles/r06_an_fwd_threshold.jsonl, r06_y_shape_audit_l3fwd.jsonl).
+constexpr uint32_t kObsMidShift = 17;
+constexpr uint32_t kObsMidMin8 = 2;
 // bit 29: more than kObsUnalignedMax of the sampled frames start off a 128-byte line (they share lines
 // with their neighbours); bit 30: the sampled lengths, rounded up to 128, span more than 128 bytes
 constexpr uint32_t kObsUnaligned = 1u << 29;

@@ -715,16 +715,18 @@ DEV void signal_done(const DoneReq& d, uint32_t nblocks) {
 
 // The footprint of a call's frames — 256 descriptors spread evenly over the call's tag & 0xFFFFFFFF
 // packets from desc (the whole call, also when it runs as sub-batches: the first sub-batch samples):
-// the mean of their lengths rounded up to 128 bytes, and how many of the 256 are longer than one
-// 8-lane row pass (kTinyRowBytes) — written to *obs (host-mapped, system scope) by one wave of the
-// launch, in one 64-bit store together with the burst's generation (tag >> 32), so the host can tell
-// a late sample of an earlier burst from this one's: kObsPresent | longs << kObsLongShift | mean. The
+// the mean of their lengths rounded up to 128 bytes, how many of the 256 are longer than one 8-lane row
+// pass (kTinyRowBytes), whether many start off a 128-byte line (kObsUnaligned), whether their rounded
+// lengths vary (kObsMixed) and how many lie between minimum and full size (kObsMidShift) — written to
+// *obs (host-mapped, system scope) by one wave of the launch, in one 64-bit store together with the
+// burst's generation (tag >> 32), so the host can tell a late sample of an earlier burst from this
+// one's: kObsPresent | bits | longs << kObsLongShift | mean (nfcs_internal.h). The
 // next call over the same burst (descriptor array, n and arena_bytes) picks its launch shape from it
 // when arena_bytes / n cannot tell (a burst inside a larger ring; a densely packed mix whose mean
 // alone says 8-lane rows; nfcs_api.hip launch_shape). Speed only.
 DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint32_t lane, uint64_t* obs) {
     const uint32_t n = (uint32_t)tag;
-    uint32_t s = 0, c = 0, u = 0, lo = 0xFFFFFFFFu, hi = 0;
+    uint32_t s = 0, c = 0, u = 0, md = 0, lo = 0xFFFFFFFFu, hi = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         const nfcs_desc d = desc[(uint32_t)(((uint64_t)(4u * lane + k) * n) >> 8)];
@@ -732,12 +734,14 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
         s += r;
         c += d.len > kTinyRowBytes ? 1u : 0u;
         u += (d.off16 & 7u) ? 1u : 0u;
+        md += (r > 128u && r <= 1408u) ? 1u : 0u;
         lo = min(lo, r);
         hi = max(hi, r);
     }
     s = row_sum<16>(s);
     c = row_sum<16>(c);
     u = row_sum<16>(u);
+    md = row_sum<16>(md);
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {  // wave min / max of the rounded lengths (one wave, once per launch)
         lo = min(lo, (uint32_t)__shfl_xor((int)lo, m));
@@ -747,8 +751,9 @@ DEV void sample_footprint(const nfcs_desc* __restrict__ desc, uint64_t tag, uint
         return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
                (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
     };
-    const uint32_t t = wave_total(s), l = wave_total(c), un = wave_total(u);
-    const uint32_t bits = (un > kObsUnalignedMax ? kObsUnaligned : 0u) | (hi - lo > 128u ? kObsMixed : 0u);
+    const uint32_t t = wave_total(s), l = wave_total(c), un = wave_total(u), mid = wave_total(md) >> 5;
+    const uint32_t bits = (un > kObsUnalignedMax ? kObsUnaligned : 0u) | (hi - lo > 128u ? kObsMixed : 0u) |
+                          ((mid < 7u ? mid : 7u) << kObsMidShift);
     if (lane == 0)
         __hip_atomic_store(obs, (tag & 0xFFFFFFFF00000000ull) | kObsPresent | bits | (l << kObsLongShift) | (t >> 8),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -423,4 +423,21 @@ call_ap() {
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/upd_threshold.jsonl --threshold 2> $o/upd_threshold.err && \
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err
 }
+call_aq() {
+  # round 6, GPU call aq: after the ring rule — the whole GPU suite, smoke(), the default bench line
+  local o=gpurun_out/r6aq; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
+call_ar() {
+  # round 6, GPU call ar: the forward keeps bimodal mixes (hardly any frames between minimum and full size,
+  # kObsMidShift) on 8-lane rows of 6 slots: slot-hint and L3 tests, the forward's threshold and main
+  # audit sets, the default line's C3 sub-lines (no host / CPU legs)
+  local o=gpurun_out/r6ar; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_l3.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_main.jsonl --l3fwd 2> $o/fwd_main.err && \
+  timeout -k 10 400 python3 -u bench.py --no-cpu --no-host --no-ops > $o/bench_mix.json 2> $o/bench_mix.err
+}
 "call_$1"
