@@ -440,4 +440,11 @@ call_ar() {
   timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_main.jsonl --l3fwd 2> $o/fwd_main.err && \
   timeout -k 10 400 python3 -u bench.py --no-cpu --no-host --no-ops > $o/bench_mix.json 2> $o/bench_mix.err
 }
+call_as() {
+  # round 6, GPU call as: after the forward's bimodal rule — the whole GPU suite, smoke(), the default line
+  local o=gpurun_out/r6as; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
 "call_$1"
