@@ -723,21 +723,25 @@ int find_burst(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc,
 // *slot = the burst's observation slot, -1 when it has none yet (the call then takes one).
 // Estimates that a sample can correct: "long" (a burst inside a larger ring), and "8-lane rows" (a
 // densely packed mix whose frames often need a second 8-lane row pass; round 6).
-bool sampled_estimate(uint64_t est) { return est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes; }
+// (the forward samples mid-size estimates too: ShapeRule::packed_rows8)
+bool sampled_estimate(uint64_t est, bool mid = false) {
+    return mid || est >= nfcs::kSmallMeanBytes || est < nfcs::kTinyMeanBytes;
+}
 // Each op's use of the sample (nfcs_internal.h, after kTinyMixMeanBytes): the mean from which a mix with
 // many long frames leaves 8-lane rows, whether mid-size frames of one length in a ring take 8-lane rows,
-// and whether a mix with hardly any mid-length frames (64 / 1500-byte traffic) stays on them.
-struct ShapeRule { uint64_t mix_mean; bool ring_rows8; bool bimodal_rows8; };
-constexpr ShapeRule kUpdateRule = {nfcs::kTinyMixMeanBytes, true, false};
-constexpr ShapeRule kFwdRule = {nfcs::kTinyMixMeanBytes, true, true};
-constexpr ShapeRule kVlanRule = {nfcs::kVlanMixMeanBytes, false, false};
+// whether a mix with hardly any mid-length frames (64 / 1500-byte traffic) stays on them, and whether
+// densely packed mid-size frames of one length on their own lines take them too (sampled for it).
+struct ShapeRule { uint64_t mix_mean; bool ring_rows8; bool bimodal_rows8; bool packed_rows8; };
+constexpr ShapeRule kUpdateRule = {nfcs::kTinyMixMeanBytes, true, false, false};
+constexpr ShapeRule kFwdRule = {nfcs::kTinyMixMeanBytes, true, true, true};
+constexpr ShapeRule kVlanRule = {nfcs::kVlanMixMeanBytes, false, false, false};
 Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, uint32_t n, int* slot,
                  const ShapeRule& rule = kUpdateRule) {
     *slot = -1;
     if (c->slot_bytes) return {c->slot_bytes, {}};
     if (n == 0) return {arena_bytes, {}};  // nothing is launched; never divide by zero
     const uint64_t est = arena_bytes / n;
-    if (!sampled_estimate(est) || !c->obs_host) return {est, {}};
+    if (!sampled_estimate(est, rule.packed_rows8) || !c->obs_host) return {est, {}};
     const int k = find_burst(c, arena_bytes, d_desc, n);
     if (k < 0) return {est, {}};
     *slot = k;
@@ -756,9 +760,10 @@ Shape peek_shape(const nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_des
         mean = nfcs::kTinyMeanBytes;
     const uint32_t bits = (uint32_t)o & (nfcs::kObsUnaligned | nfcs::kObsMixed);
     // a ring (the sample corrected a "long" estimate) of mid-size frames of one length, each on its own
-    // lines: 8-lane rows (nfcs_internal.h, after kTinyMixMeanBytes)
-    if (rule.ring_rows8 && !bits && est >= nfcs::kSmallMeanBytes && mean >= nfcs::kTinyMeanBytes &&
-        mean < nfcs::kSmallMeanBytes)
+    // lines — or, for the forward, such frames packed: 8-lane rows (nfcs_internal.h, after
+    // kTinyMixMeanBytes)
+    if (rule.ring_rows8 && !bits && (est >= nfcs::kSmallMeanBytes || rule.packed_rows8) &&
+        mean >= nfcs::kTinyMeanBytes && mean < nfcs::kSmallMeanBytes)
         mean = nfcs::kTinyMeanBytes - 1;
     return {mean, req, bits};
 }
@@ -766,7 +771,8 @@ Shape launch_shape(nfcs_ctx* c, uint64_t arena_bytes, const nfcs_desc* d_desc, u
                    const ShapeRule& rule = kUpdateRule) {
     int k = -1;
     Shape sh = peek_shape(c, arena_bytes, d_desc, n, &k, rule);
-    if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host && sampled_estimate(arena_bytes / n)) {
+    if (sh.obs.slot == nullptr && k < 0 && !c->slot_bytes && n && c->obs_host &&
+        sampled_estimate(arena_bytes / n, rule.packed_rows8)) {
         // a burst not seen lately: the least recently used slot, under a new generation
         k = 0;
         for (int j = 1; j < nfcs_ctx::kObsSlots; ++j)

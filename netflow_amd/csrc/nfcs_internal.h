@@ -92,8 +92,11 @@ constexpr uint64_t kTinyMixMeanBytes = 512;
 // rather than the short shape (nfcs_api.hip peek_shape; the update and the forward, not VLAN): round 6
 // audit, 832-1216-byte frames in 2 KiB ring slots 11-16% faster (update) and 8-13% (forward), in 4 KiB
 // slots within 3% either way (profiles/r06_y_shape_audit_threshold.jsonl, r06_an_fwd_threshold.jsonl).
-// Packed layouts of such frames are not sampled (their estimate is exact) and keep the short shape,
-// where 8-lane rows measured -5% to +11% depending on the batch.
+// Packed layouts of such frames: the update does not sample them (their estimate is exact) and keeps the
+// short shape, where 8-lane rows measured -5% to +11% depending on the batch; the forward samples them
+// and takes its 8-lane rows of 6 slots (uniform 896-1152-byte frames packed on their lines -0.5% to +12%
+// against its short-mix rows; 832-byte frames at alternating 64-byte offsets, whose sample finds them off
+// their lines, 13% slower there and keep the short-mix rows).
 // The footprint sample's 32-bit word (sample_footprint; the burst's generation in the other 32 bits).
 constexpr uint32_t kObsPresent = 0x80000000u;
 constexpr uint32_t kObsLongShift = 20;  // bits 20-28: sampled frames longer than kTinyRowBytes (0-256)

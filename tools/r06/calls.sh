@@ -447,4 +447,20 @@ call_as() {
   timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
   timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
 }
+call_at() {
+  # round 6, GPU call at: the forward samples packed mid-size bursts and runs frames of one length on their
+  # lines in 8-lane rows: slot-hint and L3 tests, the forward's main and threshold audits, the C3 sub-lines
+  local o=gpurun_out/r6at; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py tests/test_gpu_l3.py -q -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1 && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_threshold.jsonl --threshold --l3fwd 2> $o/fwd_threshold.err && \
+  timeout -k 10 400 python3 -u tools/r06/shape_audit.py $o/fwd_main.jsonl --l3fwd 2> $o/fwd_main.err && \
+  timeout -k 10 400 python3 -u bench.py --no-cpu --no-host --no-ops > $o/bench_mix.json 2> $o/bench_mix.err
+}
+call_au() {
+  # round 6, GPU call au: C3 and the forward's C3 mix on the product against the libraries at the round's
+  # start (r6start) and after the VLAN rule (vlanrule; tools/r06/build_lib_commit.sh), three alternating
+  # rounds on one box: did the round's shape rules cost the BASELINE mix lines anything?
+  local o=gpurun_out/r6au; mkdir -p $o
+  ab_lines $o 3 "cur r6start vlanrule" "c3 --config 3 --steps 40" "l3c3 --op l3fwd --config 3 --steps 40"
+}
 "call_$1"
