@@ -463,4 +463,12 @@ call_au() {
   local o=gpurun_out/r6au; mkdir -p $o
   ab_lines $o 3 "cur r6start vlanrule" "c3 --config 3 --steps 40" "l3c3 --op l3fwd --config 3 --steps 40"
 }
+call_av() {
+  # round 6, GPU call av: after the forward's packed mid-size rule — the whole GPU suite, smoke(), the
+  # default bench line
+  local o=gpurun_out/r6av; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
+  timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
+}
 "call_$1"
