@@ -471,4 +471,9 @@ call_av() {
   timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 && \
   timeout -k 10 600 python3 -u bench.py > $o/bench_default.json 2> $o/bench_default.err
 }
+call_aw() {
+  # round 6, GPU call aw: the round's evidence again on the final product (after the shape rules; same
+  # kernels for every BASELINE line): tools/r06/prof_all.sh
+  bash tools/r06/prof_all.sh r6aw
+}
 "call_$1"
