@@ -476,4 +476,10 @@ call_aw() {
   # kernels for every BASELINE line): tools/r06/prof_all.sh
   bash tools/r06/prof_all.sh r6aw
 }
+call_ax() {
+  # round 6, GPU call ax: the N > 1 line as the driver's 8-GPU run will produce it, rehearsed with 8 ranks on
+  # this one GPU (per-rank fractions and digests, host_all_ranks with 8 pinned arenas)
+  local o=gpurun_out/r6ax; mkdir -p $o
+  NFCS_BENCH_DEVICE=0 timeout -k 10 600 python3 -u bench.py --gpus 8 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus8_one_box.json 2> $o/bench_gpus8.err
+}
 "call_$1"
