@@ -408,3 +408,46 @@ def test_packed_bimodal_forward_matches_oracle(engine):
     finally:
         for b in (d_arena, d_desc, d_nh, d_tab, d_st):
             b.free()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_ring_of_mid_size_frames_runs_eight_lane_rows(engine, mixed):
+    """A burst in a ring of 2 KiB slots, no hint: arena_bytes / n says long, so the first call samples.
+    Frames of one length (1024 B) on their own lines then run 8-lane rows (footprint read back just under
+    kTinyMeanBytes; round 6 audit: 13-16% faster than the short shape), while frames of varying length
+    (U{512..1500}, same slots) keep the mean's shape. Bytes equal the oracle's at every call."""
+    n, slot = 1 << 16, 2048
+    rng = np.random.default_rng(70 + mixed)
+    lens = rng.integers(512, 1501, n) if mixed else np.full(n, 1024)
+    host = rng.integers(0, 256, size=(n, slot), dtype=np.uint8)
+    L = lens.astype(np.int64)
+    host[:, 12], host[:, 13], host[:, 14], host[:, 15] = 0x08, 0x00, 0x45, 0x00
+    host[:, 16], host[:, 17] = (L - 14) >> 8, (L - 14) & 0xFF
+    host[:, 22], host[:, 23] = 64, 17
+    host[:, 38], host[:, 39] = (L - 34) >> 8, (L - 34) & 0xFF
+    host = host.reshape(-1)
+    desc = np.zeros(n, dtype=oracle.DESC_DTYPE)
+    desc["off16"] = np.arange(n, dtype=np.uint32) * (slot // 16)
+    desc["len"] = lens
+    ref = host.copy()
+    oracle.update_batch(ref, desc, nthreads=8)
+    engine.set_slot_bytes(0)
+    # a burst is known by (descriptor array, n, arena bytes): a different arena size per case keeps the
+    # other case's sample (its descriptors may land at the same address) from being taken for this one's
+    nbytes = host.nbytes + (4096 if mixed else 0)
+    a = engine.alloc(nbytes).upload(host)
+    d = engine.alloc(desc.nbytes).upload(desc)
+    try:
+        assert engine.launch_footprint(nbytes, d, n) == nbytes // n
+        for k in range(3):
+            engine.update_device(a, nbytes, d, n)
+            engine.sync()
+            assert np.array_equal(a.download(np.uint8, host.nbytes), ref), k
+        fp = engine.launch_footprint(nbytes, d, n)
+        if mixed:
+            assert 800 <= fp < 1200, fp  # the short shape, by the mean
+        else:
+            assert fp == 799, fp  # 8-lane rows
+    finally:
+        a.free()
+        d.free()

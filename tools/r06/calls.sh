@@ -482,4 +482,9 @@ call_ax() {
   local o=gpurun_out/r6ax; mkdir -p $o
   NFCS_BENCH_DEVICE=0 timeout -k 10 600 python3 -u bench.py --gpus 8 --steps 3 --warmup 1 --no-cpu > $o/bench_gpus8_one_box.json 2> $o/bench_gpus8.err
 }
+call_ay() {
+  # round 6, GPU call ay: the slot-hint tests with the new ring-rule test
+  local o=gpurun_out/r6ay; mkdir -p $o
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py -v -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1
+}
 "call_$1"
