@@ -487,4 +487,10 @@ call_ay() {
   local o=gpurun_out/r6ay; mkdir -p $o
   timeout -k 10 400 python3 -u -m pytest tests/test_gpu_slot_hint.py -v -x --timeout 200 --timeout-method thread > $o/pytest.log 2>&1
 }
+call_az() {
+  # round 6, GPU call az: the whole GPU suite with the ring-rule test, smoke()
+  local o=gpurun_out/r6az; mkdir -p $o
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > $o/pytest_gpu.log 2>&1 && \
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1
+}
 "call_$1"
