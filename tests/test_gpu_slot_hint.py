@@ -434,11 +434,11 @@ def test_ring_of_mid_size_frames_runs_eight_lane_rows(engine, mixed):
     engine.set_slot_bytes(0)
     # a burst is known by (descriptor array, n, arena bytes): a different arena size per case keeps the
     # other case's sample (its descriptors may land at the same address) from being taken for this one's
+    # first call; from then on every call re-samples, so the footprint read back is this burst's own
     nbytes = host.nbytes + (4096 if mixed else 0)
     a = engine.alloc(nbytes).upload(host)
     d = engine.alloc(desc.nbytes).upload(desc)
     try:
-        assert engine.launch_footprint(nbytes, d, n) == nbytes // n
         for k in range(3):
             engine.update_device(a, nbytes, d, n)
             engine.sync()
